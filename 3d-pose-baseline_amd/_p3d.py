@@ -1,0 +1,162 @@
+"""ctypes binding of libp3d.so (include/p3d.h) -- the HIP hot path of the pose MLP.
+
+There is deliberately NO fallback: if the shared library is missing or fails to
+load, importing a module that needs it raises immediately.  Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (or ``make -C
+3d-pose-baseline_amd``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libp3d.so")
+
+P3D_DTYPE_F32 = 0
+P3D_DTYPE_BF16 = 1
+
+
+class P3DCfg(ctypes.Structure):
+    _fields_ = [("linear_size", c_int32), ("num_layers", c_int32), ("residual", c_int32),
+                ("batch_norm", c_int32), ("max_norm", c_int32), ("input_size", c_int32),
+                ("output_size", c_int32), ("dtype", c_int32), ("max_batch", c_int32),
+                ("bn_eps", c_float), ("bn_momentum", c_float)]
+
+
+class P3DError(RuntimeError):
+    pass
+
+
+# (name, restype, argtypes) -- exactly the entry points declared in include/p3d.h
+SIGNATURES = [
+    ("p3d_last_error", c_char_p, []),
+    ("p3d_create", c_int32, [POINTER(P3DCfg), POINTER(c_void_p)]),
+    ("p3d_destroy", c_int32, [c_void_p]),
+    ("p3d_param_count", c_int32, [c_void_p, POINTER(c_int32)]),
+    ("p3d_param_info", c_int32, [c_void_p, c_int32, POINTER(c_char_p), POINTER(c_int64),
+                                 POINTER(c_int32), POINTER(c_int64)]),
+    ("p3d_param_ptr", c_int32, [c_void_p, c_char_p, POINTER(c_void_p), POINTER(c_int64)]),
+    ("p3d_flat_ptr", c_int32, [c_void_p, c_int32, POINTER(c_void_p), POINTER(c_int64)]),
+    ("p3d_params_updated", c_int32, [c_void_p, c_void_p]),
+    ("p3d_forward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,
+                              c_uint64, c_int64, c_void_p]),
+    ("p3d_mse", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
+    ("p3d_backward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    ("p3d_adam_step", c_int32, [c_void_p, c_float, c_void_p]),
+    ("p3d_get_step", c_int32, [c_void_p, POINTER(c_int64), POINTER(c_float), POINTER(c_float)]),
+    ("p3d_set_step", c_int32, [c_void_p, c_int64, c_float, c_float]),
+    ("p3d_mpjpe_accum", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_void_p, c_void_p]),
+    ("p3d_profile_start", c_int32, [c_void_p, c_int32]),
+    ("p3d_profile_stop", c_int32, [c_void_p, c_char_p, c_int64]),
+]
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise P3DError("libp3d.so not found at %s: the HIP extension is not built "
+                       "(run __graft_entry__.build()); there is no CPU fallback" % path)
+    lib = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = load()
+    return _LIB
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().p3d_last_error().decode()
+        if rc == 1:
+            raise ValueError("%s: %s" % (what, msg))
+        raise P3DError("%s failed (%d): %s" % (what, rc, msg))
+
+
+# --------------------------------------------------------------------------------------
+# zero-copy torch views of library-owned device memory (DLPack, kDLROCM)
+# --------------------------------------------------------------------------------------
+
+
+class _DLDevice(ctypes.Structure):
+    _fields_ = [("device_type", c_int32), ("device_id", c_int32)]
+
+
+class _DLDataType(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint8), ("bits", ctypes.c_uint8), ("lanes", ctypes.c_uint16)]
+
+
+class _DLTensor(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("device", _DLDevice), ("ndim", c_int32),
+                ("dtype", _DLDataType), ("shape", POINTER(c_int64)),
+                ("strides", POINTER(c_int64)), ("byte_offset", c_uint64)]
+
+
+class _DLManagedTensor(ctypes.Structure):
+    pass
+
+
+_DELETER = ctypes.CFUNCTYPE(None, POINTER(_DLManagedTensor))
+_DLManagedTensor._fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", c_void_p),
+                             ("deleter", _DELETER)]
+
+_KEEPALIVE = {}
+_kDLROCM = 10
+
+
+@_DELETER
+def _noop_deleter(ptr):  # memory is owned by the p3d model handle
+    _KEEPALIVE.pop(ctypes.addressof(ptr.contents), None)
+
+
+def device_view(ptr: int, shape, device_index: int, dtype_code: int = 2, bits: int = 32):
+    """torch tensor aliasing ``ptr`` (no copy).  The owner must outlive the view."""
+    import torch
+    from torch.utils.dlpack import from_dlpack
+
+    shape = tuple(int(s) for s in shape)
+    shp = (c_int64 * len(shape))(*shape)
+    mt = _DLManagedTensor()
+    mt.dl_tensor.data = ptr
+    mt.dl_tensor.device = _DLDevice(_kDLROCM, device_index)
+    mt.dl_tensor.ndim = len(shape)
+    mt.dl_tensor.dtype = _DLDataType(dtype_code, bits, 1)
+    mt.dl_tensor.shape = shp
+    mt.dl_tensor.strides = None
+    mt.dl_tensor.byte_offset = 0
+    mt.manager_ctx = None
+    mt.deleter = _noop_deleter
+    _KEEPALIVE[ctypes.addressof(mt)] = (mt, shp)
+    PyCapsule_New = ctypes.pythonapi.PyCapsule_New
+    PyCapsule_New.restype = ctypes.py_object
+    PyCapsule_New.argtypes = [c_void_p, c_char_p, c_void_p]
+    cap = PyCapsule_New(ctypes.addressof(mt), b"dltensor", None)
+    t = from_dlpack(cap)
+    assert t.data_ptr() == ptr
+    return t
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (or 0 for None)."""
+    return 0 if t is None else int(t.data_ptr())
+
+
+def stream_handle(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+__all__ = ["P3DCfg", "P3DError", "lib", "check", "device_view", "ptr", "stream_handle",
+           "LIB_PATH", "SIGNATURES", "c_double"]

@@ -1,0 +1,1080 @@
+// p3d.hip -- MI355X (gfx950) kernels and the C ABI (include/p3d.h) of the 2D->3D
+// pose-lifting MLP: the hot path of EsauPR/3d-pose-baseline src/linear_model.py.
+//
+// Kernels (one launch each, all on the caller's stream):
+//   k_fwd<RS,WK>      Y = epi(X*W + b): fp32 MFMA NT-GEMM + fused epilogue
+//                     (max-norm scale, bias, BN eval|train (+moving-average update),
+//                      ReLU, Philox dropout, residual add).  linear_model.py:103-124,171-199
+//   k_dgrad<WK>       dX = dZ*W^T (+ residual grad) fused with the PREVIOUS layer's
+//                     dropout/ReLU/BN backward -> dZ_prev, dgamma, dbeta.
+//   k_wgrad           dW = X^T*dZ and db = colsum(dZ) (64x64 output tiles, LDS staged).
+//   k_adam            TF1 ApplyAdam over the flat trainable buffer.   linear_model.py:137,145
+//   k_transpose       refresh Wt = W^T after a parameter change.
+//   k_mse             loss = mean((y-t)^2), dy = 2(y-t)/(B*D).          linear_model.py:129
+//   k_mpjpe           fused un-normalize + per-joint L2 (fp64).        predict_3dpose.py:399-430
+//   k_dot_*           per-tensor reductions for --max_norm (||W||^2, <G,W>).
+#include "p3d_kernels.h"
+#include "../../include/p3d.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+// =====================================================================================
+// forward
+// =====================================================================================
+struct FwdArgs {
+  const float* X; int64_t ldx;    // [M, K]
+  const float* Wt; int64_t ldw;   // [N, K]  (transposed weight)
+  const float* bias;              // [N]
+  const float* wsq;               // max-norm: ||W||^2 (device scalar) or null
+  int M, K, N;
+  int bn;                         // 0 none, 1 eval (moving stats), 2 train (batch stats)
+  const float* gamma; const float* beta;
+  float* mmean; float* mvar;      // moving stats (read in eval, updated in train)
+  float eps; float decay;         // decay = 1 - momentum (fp32, as TF computes it)
+  float* z_save;                  // train: z = X*W + b  [M, N]
+  float* mean_save; float* var_save;
+  int relu;
+  float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
+  const float* res; int64_t ldr;  // residual added after dropout
+  float* Y; int64_t ldy;
+};
+
+// KIND only separates the symbols of the input / hidden / output layers so that
+// rocprof attributes their (very different) durations separately.
+template <int RS, int WK, int DEPTH, int KIND>
+__global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
+  __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16 * RS;
+  const int ngt = p.K >> 4;
+  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
+  f32x4 acc[RS];
+#pragma unroll
+  for (int s = 0; s < RS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_nt_core<RS, DEPTH>(p.X, p.ldx, p.M, m0, p.Wt, p.ldw, p.N, n0, gb, ge, acc);
+  if (WK > 1) {
+    if (w > 0) {
+#pragma unroll
+      for (int s = 0; s < RS; ++s) red[((w - 1) * RS + s) * 64 + lane] = acc[s];
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int u = 1; u < WK; ++u)
+#pragma unroll
+      for (int s = 0; s < RS; ++s) acc[s] += red[((u - 1) * RS + s) * 64 + lane];
+  }
+  // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r, column n0+i -------------------
+  const int i = lane & 15, q = lane >> 4;
+  const int col = n0 + i;
+  const bool cok = col < p.N;
+  const int cc = cok ? col : p.N - 1;
+  const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
+  const float b = p.bias[cc];
+  float z[RS][4];
+#pragma unroll
+  for (int s = 0; s < RS; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[s][r] = (p.wsq ? acc[s][r] / mx : acc[s][r]) + b;
+
+  float inv = 1.0f, shift = 0.0f;
+  if (p.bn) {
+    float mean, var;
+    if (p.bn == 2) {  // batch statistics over all M rows (host guarantees M <= 16*RS)
+      float sum = 0.f;
+#pragma unroll
+      for (int s = 0; s < RS; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (m0 + 16 * s + 4 * q + r < p.M) sum += z[s][r];
+      sum = p3d_colsum16(sum);
+      mean = sum / (float)p.M;
+      float sq = 0.f;
+#pragma unroll
+      for (int s = 0; s < RS; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mean; sq += d * d; }
+      sq = p3d_colsum16(sq);
+      var = sq / (float)p.M;
+      if (q == 0 && cok) {
+        p.mean_save[col] = mean;
+        p.var_save[col] = var;
+        const float mm = p.mmean[col], mv = p.mvar[col];
+        p.mmean[col] = mm - (mm - mean) * p.decay;
+        p.mvar[col] = mv - (mv - var) * p.decay;
+      }
+    } else {
+      mean = p.mmean[cc];
+      var = p.mvar[cc];
+    }
+    inv = (1.0f / sqrtf(var + p.eps)) * p.gamma[cc];
+    shift = p.beta[cc] - mean * inv;
+  }
+  if (!cok) return;
+#pragma unroll
+  for (int s = 0; s < RS; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 16 * s + 4 * q + r;
+      if (row >= p.M) continue;
+      if (p.z_save) p.z_save[(int64_t)row * p.N + col] = z[s][r];
+      float y = p.bn ? z[s][r] * inv + shift : z[s][r];
+      if (p.relu) y = fmaxf(y, 0.0f);
+      if (p.keep < 1.0f) {
+        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + row, col);
+        y = (y / p.keep) * p3d_dropout_mask(p.keep, u);
+      }
+      if (p.res) y += p.res[(int64_t)row * p.ldr + col];
+      p.Y[(int64_t)row * p.ldy + col] = y;
+    }
+}
+
+// =====================================================================================
+// data gradient + previous layer's epilogue backward
+// =====================================================================================
+struct BwdArgs {
+  const float* dZ; int64_t ldz;   // A  = dZ [M, N]
+  const float* W; int64_t ldw;    // Bt = W  [K, N] (TF layout)
+  const float* wsq;
+  int M, K, N;                    // output [M, K]
+  const float* dres; int64_t ldres;  // residual gradient added to dX (block output grad)
+  float* draw; int64_t ldraw;     // store dX (+dres) if non-null
+  int prev;                       // 1: run prev layer's dropout/relu/BN backward
+  int bn; const float* z; const float* mean; const float* var;
+  const float* gamma; const float* beta; float eps;
+  int relu; float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
+  float* dz; int64_t lddz;        // [M, K] gradient wrt prev layer's z
+  float* dgamma; float* dbeta;    // [K]
+};
+
+template <int WK, int DEPTH, int KIND>
+__global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
+  constexpr int RS = 4;
+  __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int ngt = p.N >> 4;
+  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
+  f32x4 acc[RS];
+#pragma unroll
+  for (int s = 0; s < RS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_nt_core<RS, DEPTH>(p.dZ, p.ldz, p.M, 0, p.W, p.ldw, p.K, n0, gb, ge, acc);
+  if (WK > 1) {
+    if (w > 0) {
+#pragma unroll
+      for (int s = 0; s < RS; ++s) red[((w - 1) * RS + s) * 64 + lane] = acc[s];
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int u = 1; u < WK; ++u)
+#pragma unroll
+      for (int s = 0; s < RS; ++s) acc[s] += red[((u - 1) * RS + s) * 64 + lane];
+  }
+  const int i = lane & 15, q = lane >> 4;
+  const int col = n0 + i;
+  const bool cok = col < p.K;
+  const int cc = cok ? col : p.K - 1;
+  const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
+  float g[RS][4];
+#pragma unroll
+  for (int s = 0; s < RS; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * s + 4 * q + r;
+      const int rr = row < p.M ? row : p.M - 1;
+      float d = p.wsq ? acc[s][r] / mx : acc[s][r];
+      if (p.dres) d += p.dres[(int64_t)rr * p.ldres + cc];
+      if (p.draw && cok && row < p.M) p.draw[(int64_t)row * p.ldraw + col] = d;
+      g[s][r] = d;
+    }
+  if (!p.prev) return;
+  // previous layer: y = dropout(relu(BN(z))) ; recompute a = BN(z) for the relu mask
+  float mean = 0.f, rstd = 1.f, inv = 1.f, shift = 0.f;
+  if (p.bn) {
+    mean = p.mean[cc];
+    rstd = 1.0f / sqrtf(p.var[cc] + p.eps);
+    inv = rstd * p.gamma[cc];
+    shift = p.beta[cc] - mean * inv;
+  }
+  float xh[RS][4];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int s = 0; s < RS; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * s + 4 * q + r;
+      const bool ok = row < p.M;
+      const int rr = ok ? row : p.M - 1;
+      const float zz = p.z[(int64_t)rr * p.K + cc];
+      float gg = g[s][r];
+      if (p.keep < 1.0f) {
+        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + rr, cc);
+        gg = (gg * p3d_dropout_mask(p.keep, u)) / p.keep;
+      }
+      const float a = p.bn ? zz * inv + shift : zz;
+      if (p.relu && !(a > 0.0f)) gg = 0.0f;
+      if (!ok) gg = 0.0f;
+      g[s][r] = gg;
+      const float x = (zz - mean) * rstd;
+      xh[s][r] = x;
+      sg += gg;
+      sgx += gg * x;
+    }
+  if (p.bn) {
+    sg = p3d_colsum16(sg);
+    sgx = p3d_colsum16(sgx);
+    if (q == 0 && cok) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
+  }
+  if (!cok) return;
+  const float fm = (float)p.M;
+#pragma unroll
+  for (int s = 0; s < RS; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * s + 4 * q + r;
+      if (row >= p.M) continue;
+      const float dz = p.bn ? (inv / fm) * (fm * g[s][r] - sg - xh[s][r] * sgx) : g[s][r];
+      p.dz[(int64_t)row * p.lddz + col] = dz;
+    }
+}
+
+// =====================================================================================
+// weight gradient: dW[K,N] = X^T[K,M] * dZ[M,N];  db[N] = colsum(dZ)
+// 64x64 output tile per 256-thread workgroup; wave w owns k-rows [16w,16w+16) and the
+// four 16-column subtiles.  Batch (contraction) staged through LDS in chunks of 64.
+// =====================================================================================
+struct WgradArgs {
+  const float* X; int64_t ldx;    // [M, K]
+  const float* dZ; int64_t ldz;   // [M, N]
+  int M, K, N;
+  float* dW;                      // [K, N]
+  float* db;                      // [N] or null
+};
+
+#define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
+
+__global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
+  __shared__ __attribute__((aligned(16))) float xs[64 * WG_LDS_STRIDE];
+  __shared__ __attribute__((aligned(16))) float zs[64 * WG_LDS_STRIDE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  f32x4 acc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  for (int mc = 0; mc < p.M; mc += 64) {
+    // stage X[mc..mc+64)[k0..k0+64) and dZ[mc..mc+64)[n0..n0+64)
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int m = e >> 6, c = e & 63;
+      const int gm = mc + m;
+      float xv = 0.f, zv = 0.f;
+      if (gm < p.M) {
+        if (k0 + c < p.K) xv = p.X[(int64_t)gm * p.ldx + k0 + c];
+        if (n0 + c < p.N) zv = p.dZ[(int64_t)gm * p.ldz + n0 + c];
+      }
+      xs[m * WG_LDS_STRIDE + c] = xv;
+      zs[m * WG_LDS_STRIDE + c] = zv;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const int m = 4 * t + q;
+      const float a = xs[m * WG_LDS_STRIDE + 16 * w + i];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[m * WG_LDS_STRIDE + 16 * s + i], acc[s], 0, 0, 0);
+    }
+    if (p.db && blockIdx.y == 0 && tid < 64) {
+      for (int m = 0; m < 64; ++m) dbs += zs[m * WG_LDS_STRIDE + tid];
+    }
+    __syncthreads();
+  }
+  if (p.db && blockIdx.y == 0 && tid < 64 && n0 + tid < p.N) p.db[n0 + tid] = dbs;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 16 * w + 4 * q + r;
+      const int n = n0 + 16 * s + i;
+      if (k < p.K && n < p.N) p.dW[(int64_t)k * p.N + n] = acc[s][r];
+    }
+}
+
+// =====================================================================================
+// TF1 ApplyAdam over the flat trainable buffer (float4 vectorised)
+// =====================================================================================
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ w, float* __restrict__ m,
+                                              float* __restrict__ v, const float* __restrict__ g,
+                                              int64_t n4, float alpha, float one_m_b1, float one_m_b2,
+                                              float eps) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = idx; e < n4; e += stride) {
+    f32x4 gg = ((const f32x4*)g)[e];
+    f32x4 mm = ((f32x4*)m)[e];
+    f32x4 vv = ((f32x4*)v)[e];
+    f32x4 ww = ((f32x4*)w)[e];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mm[c] += (gg[c] - mm[c]) * one_m_b1;
+      vv[c] += (gg[c] * gg[c] - vv[c]) * one_m_b2;
+      ww[c] -= (mm[c] * alpha) / (sqrtf(vv[c]) + eps);
+    }
+    ((f32x4*)m)[e] = mm;
+    ((f32x4*)v)[e] = vv;
+    ((f32x4*)w)[e] = ww;
+  }
+}
+
+// =====================================================================================
+// transpose W [R, C] -> Wt [C, R] for every weight tensor (one launch)
+// =====================================================================================
+#define P3D_MAX_W 40
+struct TransTable {
+  int n;
+  int rows[P3D_MAX_W], cols[P3D_MAX_W];
+  int tile_begin[P3D_MAX_W + 1];
+  int64_t src[P3D_MAX_W], dst[P3D_MAX_W];  // element offsets into params / wt buffers
+};
+
+__global__ __launch_bounds__(256) void k_transpose(const float* __restrict__ params, float* __restrict__ wt,
+                                                   TransTable tt) {
+  __shared__ float tile[32][33];
+  int t = 0;
+  while (t + 1 < tt.n && (int)blockIdx.x >= tt.tile_begin[t + 1]) ++t;
+  const int R = tt.rows[t], C = tt.cols[t];
+  const int local = blockIdx.x - tt.tile_begin[t];
+  const int tc = (C + 31) / 32;
+  const int r0 = (local / tc) * 32, c0 = (local % tc) * 32;
+  const float* src = params + tt.src[t];
+  float* dst = wt + tt.dst[t];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < R && c < C) ? src[(int64_t)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < C && r < R) dst[(int64_t)c * R + r] = tile[tx][y];
+  }
+}
+
+// =====================================================================================
+// MSE loss + gradient (single workgroup; deterministic)
+// =====================================================================================
+__global__ __launch_bounds__(256) void k_mse(const float* __restrict__ y, const float* __restrict__ t,
+                                             int64_t n, float* loss, float* dy) {
+  __shared__ float part[256];
+  const float invn = 1.0f / (float)n;
+  float s = 0.f;
+  for (int64_t e = threadIdx.x; e < n; e += 256) {
+    const float d = y[e] - t[e];
+    s += d * d;
+    if (dy) dy[e] = invn * (d * 2.0f);
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && loss) *loss = part[0] / (float)n;
+}
+
+// =====================================================================================
+// MPJPE: un-normalize (fp64) + per-joint L2 of 17 joints, accumulated into joint_sum[17]
+// Bit-for-bit the per-frame arithmetic of predict_3dpose.py:399-430 (no FMA contraction).
+// =====================================================================================
+__global__ __launch_bounds__(256) void k_mpjpe(const float* __restrict__ pred, const float* __restrict__ gt,
+                                               const double* __restrict__ mean, const double* __restrict__ stdv,
+                                               const int32_t* __restrict__ dims, int64_t B, double* joint_sum) {
+  __shared__ double part[16][257];
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int j = 0; j < 16; ++j) {
+    double dist = 0.0;
+    if (f < B) {
+      double sq[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int c = 3 * j + d;
+        const int idx = dims[c];
+        const double pv = __dadd_rn(__dmul_rn((double)pred[f * 48 + c], stdv[idx]), mean[idx]);
+        const double gv = __dadd_rn(__dmul_rn((double)gt[f * 48 + c], stdv[idx]), mean[idx]);
+        const double df = __dsub_rn(pv, gv);
+        sq[d] = __dmul_rn(df, df);
+      }
+      dist = sqrt(__dadd_rn(__dadd_rn(sq[0], sq[1]), sq[2]));
+    }
+    part[j][threadIdx.x] = dist;
+  }
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+      for (int j = 0; j < 16; ++j) part[j][threadIdx.x] += part[j][threadIdx.x + h];
+    __syncthreads();
+  }
+  // joint 0 (root) is mean-vs-mean: distance exactly 0, nothing to add
+  if (threadIdx.x < 16) atomicAdd(joint_sum + 1 + threadIdx.x, part[threadIdx.x][0]);
+}
+
+// =====================================================================================
+// per-tensor dot products (max-norm): out[t] = sum a_t * b_t   (two deterministic passes)
+// =====================================================================================
+struct DotTable {
+  int n;
+  int64_t off[P3D_MAX_W];
+  int64_t len[P3D_MAX_W];
+};
+
+#define DOT_CHUNKS 64
+__global__ __launch_bounds__(256) void k_dot_partial(const float* __restrict__ a, const float* __restrict__ b,
+                                                     DotTable tb, float* __restrict__ part) {
+  __shared__ float s[256];
+  const int t = blockIdx.y;
+  const float* pa = a + tb.off[t];
+  const float* pb = b + tb.off[t];
+  float acc = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tb.len[t]; e += (int64_t)DOT_CHUNKS * 256)
+    acc += pa[e] * pb[e];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) s[threadIdx.x] += s[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[t * DOT_CHUNKS + blockIdx.x] = s[0];
+}
+
+__global__ void k_dot_final(const float* __restrict__ part, int n, float* __restrict__ out) {
+  const int t = threadIdx.x;
+  if (t >= n) return;
+  float acc = 0.f;
+  for (int c = 0; c < DOT_CHUNKS; ++c) acc += part[t * DOT_CHUNKS + c];
+  out[t] = acc;
+}
+
+// max-norm gradient: g = G/m - [n>=1] <G,W> W / (m^2 n), n = ||W||, m = max(n,1)
+__global__ __launch_bounds__(256) void k_maxnorm_grad(float* __restrict__ g, const float* __restrict__ w,
+                                                      DotTable tb, const float* __restrict__ wsq,
+                                                      const float* __restrict__ gw) {
+  const int t = blockIdx.y;
+  const float n = sqrtf(wsq[t]);
+  const float m = fmaxf(n, 1.0f);
+  const float c = n >= 1.0f ? gw[t] / (m * m * n) : 0.0f;
+  float* pg = g + tb.off[t];
+  const float* pw = w + tb.off[t];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tb.len[t]; e += (int64_t)gridDim.x * 256)
+    pg[e] = pg[e] / m - c * pw[e];
+}
+
+// =====================================================================================
+// host side
+// =====================================================================================
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) return fail(P3D_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define LAUNCH_CHECK(what)                                                          \
+  do {                                                                              \
+    hipError_t e_ = hipGetLastError();                                              \
+    if (e_ != hipSuccess) return fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
+
+struct Tensor {
+  std::string name;
+  int64_t numel;
+  int64_t off;   // element offset (flat trainable buffer, or moving buffer for kind 1)
+  int kind;      // 0 trainable, 1 moving stat
+};
+
+struct Layer {
+  int K, N;
+  int64_t w, b, gamma = -1, beta = -1;  // offsets in params
+  int64_t mmean = -1, mvar = -1;        // offsets in moving
+  int64_t wt;                           // offset in wt buffer
+  int widx;                             // weight index (max-norm tables)
+  int site;                             // dropout site; -1 for the output layer
+  bool bn, relu;
+};
+
+}  // namespace
+
+struct p3d_model {
+  p3d_cfg cfg;
+  std::vector<Tensor> tensors;
+  std::vector<Layer> layers;  // in, A0, B0, ..., out
+  int64_t n_flat = 0, n_moving = 0, n_wt = 0;
+  float* flat[4] = {nullptr, nullptr, nullptr, nullptr};  // params, grads, m, v
+  float* moving = nullptr;
+  float* wt = nullptr;
+  float* ws = nullptr;        // activation workspace
+  int64_t ws_elems = 0;
+  float* scratch = nullptr;   // reductions (max-norm)
+  float* wsq = nullptr;       // [nW] ||W||^2
+  float* gw = nullptr;        // [nW] <G,W>
+  TransTable tt;
+  DotTable wtab;
+  // per-layer workspace pointers (B_max rows)
+  std::vector<float*> act;    // output of layer l (block layer B_i holds the block output)
+  std::vector<float*> z;      // pre-BN z of layer l
+  std::vector<float*> bmean, bvar;
+  std::vector<float*> dz;     // gradient wrt z of layer l
+  float* dout[2] = {nullptr, nullptr};
+  // training cache
+  bool have_cache = false;
+  const float* x_cached = nullptr;
+  int64_t B_cached = 0;
+  float keep = 1.f;
+  uint64_t seed = 0, ctr = 0;
+  int64_t row_off = 0;
+  int64_t global_step = 0;
+  float b1p = 0.9f, b2p = 0.999f;
+  // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
+  bool prof = false;
+  std::vector<hipEvent_t> ev;
+  std::vector<const char*> ev_tag;
+  size_t ev_used = 0;
+};
+
+namespace {
+struct ProfScope {  // brackets one kernel launch with an event pair when profiling
+  p3d_model* m; hipStream_t st; bool on;
+  ProfScope(p3d_model* m_, const char* tag, hipStream_t st_) : m(m_), st(st_), on(false) {
+    if (m && m->prof && 2 * (m->ev_used + 1) <= m->ev.size()) {
+      on = true;
+      m->ev_tag[m->ev_used] = tag;
+      (void)hipEventRecord(m->ev[2 * m->ev_used], st);
+    }
+  }
+  ~ProfScope() {
+    if (on) { (void)hipEventRecord(m->ev[2 * m->ev_used + 1], st); ++m->ev_used; }
+  }
+};
+}  // namespace
+
+extern "C" const char* p3d_last_error(void) { return g_err.c_str(); }
+
+static int layer_count(const p3d_cfg& c) { return 2 + 2 * c.num_layers; }
+
+extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
+  if (!cfg_in || !out) return fail(P3D_ERR_ARG, "p3d_create: null argument");
+  const p3d_cfg c = *cfg_in;
+  if (c.linear_size <= 0 || c.linear_size % 16 != 0)
+    return fail(P3D_ERR_ARG, "linear_size must be a positive multiple of 16");
+  if (c.num_layers < 0) return fail(P3D_ERR_ARG, "num_layers must be >= 0");
+  if (c.input_size <= 0 || c.input_size % 16 != 0)
+    return fail(P3D_ERR_ARG, "input_size must be a positive multiple of 16");
+  if (c.output_size <= 0) return fail(P3D_ERR_ARG, "output_size must be positive");
+  if (c.max_batch <= 0) return fail(P3D_ERR_ARG, "max_batch must be positive");
+  if (c.dtype != P3D_DTYPE_F32) return fail(P3D_ERR_ARG, "only P3D_DTYPE_F32 models in this build");
+  p3d_model* m = new p3d_model();
+  m->cfg = c;
+  const int L = c.linear_size;
+  const int OUTP = (c.output_size + 15) / 16 * 16;  // padded output features (Wt rows)
+  (void)OUTP;
+  auto add = [&](const std::string& name, int64_t n) {
+    Tensor t{name, n, m->n_flat, 0};
+    m->n_flat += pad64(n);
+    m->tensors.push_back(t);
+    return t.off;
+  };
+  auto addm = [&](const std::string& name, int64_t n) {
+    Tensor t{name, n, m->n_moving, 1};
+    m->n_moving += pad64(n);
+    m->tensors.push_back(t);
+    return t.off;
+  };
+  // trainables in TF creation order (linear_model.py:103-124, 171-193)
+  std::vector<std::string> bn_scope;
+  Layer lin{};
+  lin.K = c.input_size; lin.N = L; lin.site = 0; lin.bn = c.batch_norm; lin.relu = true;
+  lin.w = add("linear_model/w1", (int64_t)c.input_size * L);
+  lin.b = add("linear_model/b1", L);
+  if (c.batch_norm) {
+    lin.gamma = add("linear_model/batch_normalization/gamma", L);
+    lin.beta = add("linear_model/batch_normalization/beta", L);
+    bn_scope.push_back("linear_model/batch_normalization");
+  }
+  m->layers.push_back(lin);
+  for (int i = 0; i < c.num_layers; ++i) {
+    const std::string s = "linear_model/two_linear_" + std::to_string(i) + "/";
+    for (int h = 0; h < 2; ++h) {
+      Layer ly{};
+      ly.K = L; ly.N = L; ly.site = 1 + 2 * i + h; ly.bn = c.batch_norm; ly.relu = true;
+      const std::string wn = (h == 0 ? "w2_" : "w3_") + std::to_string(i);
+      const std::string bnm = (h == 0 ? "b2_" : "b3_") + std::to_string(i);
+      ly.w = add(s + wn, (int64_t)L * L);
+      ly.b = add(s + bnm, L);
+      if (c.batch_norm) {
+        const std::string sc = s + "batch_normalization" + std::to_string(h + 1) + std::to_string(i);
+        ly.gamma = add(sc + "/gamma", L);
+        ly.beta = add(sc + "/beta", L);
+        bn_scope.push_back(sc);
+      }
+      m->layers.push_back(ly);
+    }
+  }
+  Layer lo{};
+  lo.K = L; lo.N = c.output_size; lo.site = -1; lo.bn = false; lo.relu = false;
+  lo.w = add("linear_model/w4", (int64_t)L * c.output_size);
+  lo.b = add("linear_model/b4", c.output_size);
+  m->layers.push_back(lo);
+  // moving statistics (non-trainable)
+  if (c.batch_norm) {
+    for (size_t l = 0; l + 1 < m->layers.size(); ++l) {
+      m->layers[l].mmean = addm(bn_scope[l] + "/moving_mean", L);
+      m->layers[l].mvar = addm(bn_scope[l] + "/moving_variance", L);
+    }
+  }
+  // transposed-weight buffer and tables
+  m->tt.n = 0;
+  m->wtab.n = 0;
+  int tiles = 0;
+  for (size_t l = 0; l < m->layers.size(); ++l) {
+    Layer& ly = m->layers[l];
+    const int K = ly.K, N = ly.N;
+    ly.wt = m->n_wt;
+    const int NP = (N + 15) / 16 * 16;
+    m->n_wt += pad64((int64_t)NP * K);
+    const int t = m->tt.n++;
+    if (t >= P3D_MAX_W) { delete m; return fail(P3D_ERR_ARG, "too many layers"); }
+    m->tt.rows[t] = K; m->tt.cols[t] = N;
+    m->tt.src[t] = ly.w; m->tt.dst[t] = ly.wt;
+    m->tt.tile_begin[t] = tiles;
+    tiles += ((K + 31) / 32) * ((N + 31) / 32);
+    ly.widx = t;
+    m->wtab.off[t] = ly.w;
+    m->wtab.len[t] = (int64_t)K * N;
+    m->wtab.n = t + 1;
+  }
+  m->tt.tile_begin[m->tt.n] = tiles;
+
+  auto cleanup = [&](hipError_t e) {
+    g_err = std::string("p3d_create: ") + hipGetErrorString(e);
+    for (auto& p : m->flat) if (p) (void)hipFree(p);
+    if (m->moving) (void)hipFree(m->moving);
+    if (m->wt) (void)hipFree(m->wt);
+    if (m->ws) (void)hipFree(m->ws);
+    if (m->scratch) (void)hipFree(m->scratch);
+    delete m;
+    return P3D_ERR_HIP;
+  };
+  hipError_t e;
+  for (int k = 0; k < 4; ++k) {
+    if ((e = hipMalloc(&m->flat[k], m->n_flat * sizeof(float))) != hipSuccess) return cleanup(e);
+    if ((e = hipMemset(m->flat[k], 0, m->n_flat * sizeof(float))) != hipSuccess) return cleanup(e);
+  }
+  if ((e = hipMalloc(&m->moving, (m->n_moving + 64) * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->moving, 0, (m->n_moving + 64) * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMalloc(&m->wt, m->n_wt * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->wt, 0, m->n_wt * sizeof(float))) != hipSuccess) return cleanup(e);
+  // workspace: per layer act, z, dz ([Bmax, N]); per layer stats; dout x2
+  const int64_t Bm = c.max_batch;
+  const int nl = (int)m->layers.size();
+  int64_t need = 0;
+  for (int l = 0; l < nl - 1; ++l) need += 3 * pad64(Bm * L) + 2 * pad64(L);
+  need += 2 * pad64(Bm * L);
+  m->ws_elems = need;
+  if ((e = hipMalloc(&m->ws, need * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->ws, 0, need * sizeof(float))) != hipSuccess) return cleanup(e);
+  float* cur = m->ws;
+  m->act.assign(nl, nullptr); m->z.assign(nl, nullptr); m->dz.assign(nl, nullptr);
+  m->bmean.assign(nl, nullptr); m->bvar.assign(nl, nullptr);
+  for (int l = 0; l < nl - 1; ++l) {
+    m->act[l] = cur; cur += pad64(Bm * L);
+    m->z[l] = cur; cur += pad64(Bm * L);
+    m->dz[l] = cur; cur += pad64(Bm * L);
+    m->bmean[l] = cur; cur += pad64(L);
+    m->bvar[l] = cur; cur += pad64(L);
+  }
+  m->dout[0] = cur; cur += pad64(Bm * L);
+  m->dout[1] = cur; cur += pad64(Bm * L);
+  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
+  if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
+  m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
+  m->gw = m->wsq + 64;
+  // TF defaults: BN gamma = 1, moving_variance = 1 (beta/mean = 0 already)
+  if (c.batch_norm) {
+    std::vector<float> ones(L, 1.0f);
+    for (int l = 0; l < nl - 1; ++l) {
+      if ((e = hipMemcpy(m->flat[0] + m->layers[l].gamma, ones.data(), L * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(e);
+      if ((e = hipMemcpy(m->moving + m->layers[l].mvar, ones.data(), L * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(e);
+    }
+  }
+  *out = m;
+  return P3D_OK;
+}
+
+extern "C" int p3d_destroy(p3d_model* m) {
+  if (!m) return P3D_OK;
+  for (auto e : m->ev) (void)hipEventDestroy(e);
+  for (auto& p : m->flat) if (p) (void)hipFree(p);
+  if (m->moving) (void)hipFree(m->moving);
+  if (m->wt) (void)hipFree(m->wt);
+  if (m->ws) (void)hipFree(m->ws);
+  if (m->scratch) (void)hipFree(m->scratch);
+  delete m;
+  return P3D_OK;
+}
+
+extern "C" int p3d_param_count(const p3d_model* m, int32_t* count) {
+  if (!m || !count) return fail(P3D_ERR_ARG, "null argument");
+  *count = (int32_t)m->tensors.size();
+  return P3D_OK;
+}
+
+extern "C" int p3d_param_info(const p3d_model* m, int32_t idx, const char** name, int64_t* numel,
+                              int32_t* kind, int64_t* offset) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  if (idx < 0 || idx >= (int32_t)m->tensors.size()) return fail(P3D_ERR_ARG, "param index out of range");
+  const Tensor& t = m->tensors[idx];
+  if (name) *name = t.name.c_str();
+  if (numel) *numel = t.numel;
+  if (kind) *kind = t.kind;
+  if (offset) *offset = t.off;
+  return P3D_OK;
+}
+
+extern "C" int p3d_param_ptr(p3d_model* m, const char* name, void** dptr, int64_t* numel) {
+  if (!m || !name || !dptr) return fail(P3D_ERR_ARG, "null argument");
+  for (const Tensor& t : m->tensors) {
+    if (t.name == name) {
+      *dptr = (t.kind == 0 ? m->flat[0] : m->moving) + t.off;
+      if (numel) *numel = t.numel;
+      return P3D_OK;
+    }
+  }
+  return fail(P3D_ERR_NOTFOUND, std::string("unknown parameter: ") + name);
+}
+
+extern "C" int p3d_flat_ptr(p3d_model* m, int32_t which, void** dptr, int64_t* numel) {
+  if (!m || !dptr) return fail(P3D_ERR_ARG, "null argument");
+  if (which >= 0 && which < 4) {
+    *dptr = m->flat[which];
+    if (numel) *numel = m->n_flat;
+    return P3D_OK;
+  }
+  if (which == 4) {
+    *dptr = m->moving;
+    if (numel) *numel = m->n_moving;
+    return P3D_OK;
+  }
+  return fail(P3D_ERR_ARG, "p3d_flat_ptr: which must be 0..4");
+}
+
+static int refresh_derived(p3d_model* m, hipStream_t st) {
+  const int tiles = m->tt.tile_begin[m->tt.n];
+  {
+    ProfScope ps(m, "transpose", st);
+    k_transpose<<<tiles, 256, 0, st>>>(m->flat[0], m->wt, m->tt);
+  }
+  LAUNCH_CHECK("k_transpose");
+  if (m->cfg.max_norm) {
+    k_dot_partial<<<dim3(DOT_CHUNKS, m->wtab.n), 256, 0, st>>>(m->flat[0], m->flat[0], m->wtab, m->scratch);
+    LAUNCH_CHECK("k_dot_partial");
+    k_dot_final<<<1, 64, 0, st>>>(m->scratch, m->wtab.n, m->wsq);
+    LAUNCH_CHECK("k_dot_final");
+  }
+  return P3D_OK;
+}
+
+extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  return refresh_derived(m, (hipStream_t)stream);
+}
+
+// ---- launch helpers ------------------------------------------------------------------
+template <int KIND>
+static void launch_fwd_k(const FwdArgs& a, bool whole_batch, hipStream_t st) {
+  const int gx = (a.N + 15) / 16;
+  if (whole_batch) {  // BN-train: one workgroup owns all rows of its 16 columns
+    k_fwd<4, 4, 3, KIND><<<dim3(gx, 1), 256, 0, st>>>(a);
+  } else {
+    const int gy = (a.M + 15) / 16;
+    k_fwd<1, 4, 8, KIND><<<dim3(gx, gy), 256, 0, st>>>(a);
+  }
+}
+
+static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch, hipStream_t st) {
+  static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
+                                   {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
+  ProfScope ps(m, tags[whole_batch ? 1 : 0][kind], st);
+  if (kind == 0) launch_fwd_k<0>(a, whole_batch, st);
+  else if (kind == 1) launch_fwd_k<1>(a, whole_batch, st);
+  else launch_fwd_k<2>(a, whole_batch, st);
+  LAUNCH_CHECK("k_fwd");
+  return P3D_OK;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
+                           float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, void* stream) {
+  if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_forward: null argument");
+  const p3d_cfg& c = m->cfg;
+  if (B <= 0) return fail(P3D_ERR_ARG, "p3d_forward: batch must be positive");
+  if (B > c.max_batch)
+    return fail(P3D_ERR_ARG, "p3d_forward: batch " + std::to_string(B) + " exceeds max_batch " +
+                                 std::to_string(c.max_batch));
+  if (training && c.batch_norm && B > 64)
+    return fail(P3D_ERR_ARG, "p3d_forward: training with batch_norm supports B <= 64 in this build");
+  if (!(keep_prob > 0.f && keep_prob <= 1.f)) return fail(P3D_ERR_ARG, "keep_prob must be in (0, 1]");
+  if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_forward: x must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int L = c.linear_size;
+  const float decay = 1.0f - c.bn_momentum;
+  const int nl = (int)m->layers.size();
+  const float* in = x;
+  int64_t ldin = c.input_size;
+  for (int l = 0; l < nl; ++l) {
+    const Layer& ly = m->layers[l];
+    FwdArgs a{};
+    a.X = in; a.ldx = ldin;
+    a.Wt = m->wt + ly.wt; a.ldw = ly.K;
+    a.bias = m->flat[0] + ly.b;
+    a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
+    a.M = (int)B; a.K = ly.K; a.N = ly.N;
+    const bool last = (l == nl - 1);
+    if (ly.bn) {
+      a.bn = training ? 2 : 1;
+      a.gamma = m->flat[0] + ly.gamma; a.beta = m->flat[0] + ly.beta;
+      a.mmean = m->moving + ly.mmean; a.mvar = m->moving + ly.mvar;
+      a.eps = c.bn_eps; a.decay = decay;
+      if (training) { a.mean_save = m->bmean[l]; a.var_save = m->bvar[l]; }
+    }
+    if (training && !last) a.z_save = m->z[l];
+    a.relu = ly.relu;
+    a.keep = last ? 1.0f : keep_prob;
+    a.seed = seed; a.ctr = ctr; a.site = ly.site; a.row_off = row_offset;
+    // residual: second layer of block i adds the block input (layer l-2's output)
+    const bool second = (l >= 1 && !last && ((l - 1) % 2 == 1));
+    if (c.residual && second) { a.res = (l - 2 >= 0) ? m->act[l - 2] : nullptr; a.ldr = L; }
+    if (last) { a.Y = y; a.ldy = ly.N; }
+    else { a.Y = m->act[l]; a.ldy = L; }
+    const int kind = (l == 0) ? 0 : (last ? 2 : 1);
+    const int rc = launch_fwd(m, a, kind, training && ly.bn, st);
+    if (rc) return rc;
+    in = a.Y; ldin = a.ldy;
+  }
+  if (training) {
+    m->have_cache = true;
+    m->x_cached = x;
+    m->B_cached = B;
+    m->keep = keep_prob;
+    m->seed = seed; m->ctr = ctr; m->row_off = row_offset;
+  }
+  return P3D_OK;
+}
+
+extern "C" int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, float* loss_dev, float* dy,
+                       void* stream) {
+  if (!y || !t) return fail(P3D_ERR_ARG, "p3d_mse: null argument");
+  if (B <= 0 || D <= 0) return fail(P3D_ERR_ARG, "p3d_mse: bad shape");
+  k_mse<<<1, 256, 0, (hipStream_t)stream>>>(y, t, B * D, loss_dev, dy);
+  LAUNCH_CHECK("k_mse");
+  return P3D_OK;
+}
+
+static int launch_wgrad(p3d_model* m, const float* X, int64_t ldx, const float* dZ, int64_t ldz, int M, int K,
+                        int N, float* dW, float* db, hipStream_t st) {
+  WgradArgs a{X, ldx, dZ, ldz, M, K, N, dW, db};
+  ProfScope ps(m, "wgrad", st);
+  k_wgrad<<<dim3((N + 63) / 64, (K + 63) / 64), 256, 0, st>>>(a);
+  LAUNCH_CHECK("k_wgrad");
+  return P3D_OK;
+}
+
+extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stream) {
+  if (!m || !dy) return fail(P3D_ERR_ARG, "p3d_backward: null argument");
+  if (!m->have_cache) return fail(P3D_ERR_STATE, "p3d_backward: no training forward to differentiate");
+  if (B != m->B_cached) return fail(P3D_ERR_ARG, "p3d_backward: batch differs from the training forward");
+  if (B > 64) return fail(P3D_ERR_ARG, "p3d_backward: B <= 64 in this build");
+  const p3d_cfg& c = m->cfg;
+  hipStream_t st = (hipStream_t)stream;
+  const int L = c.linear_size;
+  const int nl = (int)m->layers.size();
+  float* grads = m->flat[1];
+  const float* params = m->flat[0];
+  // layer l's input activation
+  auto input_of = [&](int l) -> const float* { return l == 0 ? m->x_cached : m->act[l - 1]; };
+  auto ld_in = [&](int l) -> int64_t { return l == 0 ? c.input_size : L; };
+  // Walk layers from the output back.  grad_in = gradient wrt layer l's z.
+  const float* dz_cur = dy;      // gradient wrt z of current layer l
+  int64_t ldz_cur = c.output_size;
+  int dsel = 0;
+  const float* dres_next = nullptr;  // block-output gradient to add when differentiating A-layer
+  for (int l = nl - 1; l >= 0; --l) {
+    const Layer& ly = m->layers[l];
+    // weight gradient of layer l
+    int rc = launch_wgrad(m, input_of(l), ld_in(l), dz_cur, ldz_cur, (int)B, ly.K, ly.N, grads + ly.w, grads + ly.b, st);
+    if (rc) return rc;
+    if (l == 0) break;
+    // data gradient into layer l-1
+    const Layer& pv = m->layers[l - 1];
+    BwdArgs a{};
+    a.dZ = dz_cur; a.ldz = ldz_cur;
+    a.W = params + ly.w; a.ldw = ly.N;
+    a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
+    a.M = (int)B; a.K = ly.K; a.N = ly.N;
+    const bool is_out = (l == nl - 1);
+    const bool is_A = !is_out && ((l - 1) % 2 == 0);   // first layer of a block
+    // the output of layer l-1 is a block output when l-1 is a B-layer (or the input layer)
+    if (c.residual) {
+      if (is_out) {  // d(last block out): store raw for the block's residual
+        a.draw = m->dout[dsel]; a.ldraw = L;
+      } else if (is_A) {  // dX of a block input = dZ*W^T + d(block output)
+        a.dres = dres_next; a.ldres = L;
+        if (l - 1 >= 1) { a.draw = m->dout[dsel]; a.ldraw = L; }
+      }
+    }
+    a.prev = 1;
+    a.bn = pv.bn;
+    a.z = m->z[l - 1]; a.mean = m->bmean[l - 1]; a.var = m->bvar[l - 1];
+    if (pv.bn) { a.gamma = params + pv.gamma; a.beta = params + pv.beta; }
+    a.eps = c.bn_eps;
+    a.relu = pv.relu;
+    a.keep = m->keep; a.seed = m->seed; a.ctr = m->ctr; a.site = pv.site; a.row_off = m->row_off;
+    a.dz = m->dz[l - 1]; a.lddz = L;
+    if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
+    if ((a.N % 16) != 0 || !aligned16(a.dZ) || (a.ldz % 4) != 0 || (a.ldw % 4) != 0)
+      return fail(P3D_ERR_ARG, "p3d_backward: output_size must be a multiple of 16 in this build");
+    {
+      ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden", st);
+      if (is_out) k_dgrad<4, 3, 2><<<dim3((a.K + 15) / 16, 1), 256, 0, st>>>(a);
+      else k_dgrad<4, 3, 1><<<dim3((a.K + 15) / 16, 1), 256, 0, st>>>(a);
+    }
+    LAUNCH_CHECK("k_dgrad");
+    if (a.draw) { dres_next = a.draw; dsel ^= 1; }
+    dz_cur = m->dz[l - 1];
+    ldz_cur = L;
+  }
+  if (c.max_norm) {
+    // G (dL/dW_eff) -> dL/dW through clip_by_norm
+    k_dot_partial<<<dim3(DOT_CHUNKS, m->wtab.n), 256, 0, st>>>(grads, params, m->wtab, m->scratch);
+    LAUNCH_CHECK("k_dot_partial");
+    k_dot_final<<<1, 64, 0, st>>>(m->scratch, m->wtab.n, m->gw);
+    LAUNCH_CHECK("k_dot_final");
+    k_maxnorm_grad<<<dim3(64, m->wtab.n), 256, 0, st>>>(grads, params, m->wtab, m->wsq, m->gw);
+    LAUNCH_CHECK("k_maxnorm_grad");
+  }
+  return P3D_OK;
+}
+
+extern "C" int p3d_adam_step(p3d_model* m, float lr, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  hipStream_t st = (hipStream_t)stream;
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+  // alpha in fp32 exactly as TF's ApplyAdam functor computes it
+  const float alpha = lr * sqrtf(1.0f - m->b2p) / (1.0f - m->b1p);
+  const int64_t n4 = m->n_flat / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  {
+    ProfScope ps(m, "adam", st);
+  k_adam<<<blocks, 256, 0, st>>>(m->flat[0], m->flat[2], m->flat[3], m->flat[1], n4, alpha, 1.0f - b1, 1.0f - b2, eps);
+  }
+  LAUNCH_CHECK("k_adam");
+  m->b1p = m->b1p * b1;
+  m->b2p = m->b2p * b2;
+  m->global_step += 1;
+  return refresh_derived(m, st);
+}
+
+extern "C" int p3d_get_step(const p3d_model* m, int64_t* gs, float* b1p, float* b2p) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  if (gs) *gs = m->global_step;
+  if (b1p) *b1p = m->b1p;
+  if (b2p) *b2p = m->b2p;
+  return P3D_OK;
+}
+
+extern "C" int p3d_set_step(p3d_model* m, int64_t gs, float b1p, float b2p) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  m->global_step = gs;
+  m->b1p = b1p;
+  m->b2p = b2p;
+  return P3D_OK;
+}
+
+extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96,
+                               const double* std96, const int32_t* dims48, int64_t B, double* joint_sum17,
+                               void* stream) {
+  if (!pred_n || !gt_n || !mean96 || !std96 || !dims48 || !joint_sum17)
+    return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: null argument");
+  if (B <= 0) return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: batch must be positive");
+  k_mpjpe<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred_n, gt_n, mean96, std96, dims48, B,
+                                                                         joint_sum17);
+  LAUNCH_CHECK("k_mpjpe");
+  return P3D_OK;
+}
+
+extern "C" int p3d_profile_start(p3d_model* m, int32_t max_launches) {
+  if (!m || max_launches <= 0) return fail(P3D_ERR_ARG, "p3d_profile_start: bad argument");
+  for (auto e : m->ev) (void)hipEventDestroy(e);
+  m->ev.assign(2 * (size_t)max_launches, nullptr);
+  m->ev_tag.assign((size_t)max_launches, nullptr);
+  for (auto& e : m->ev) HIP_TRY(hipEventCreate(&e));
+  m->ev_used = 0;
+  m->prof = true;
+  return P3D_OK;
+}
+
+// Synchronises, then writes "tag<TAB>count<TAB>total_us<TAB>min_us<TAB>max_us\n" per tag.
+extern "C" int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  m->prof = false;
+  std::vector<std::string> tags;
+  std::vector<double> tot, mn, mx;
+  std::vector<int64_t> cnt;
+  for (size_t k = 0; k < m->ev_used; ++k) {
+    HIP_TRY(hipEventSynchronize(m->ev[2 * k + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, m->ev[2 * k], m->ev[2 * k + 1]));
+    const double us = 1000.0 * ms;
+    size_t t = 0;
+    while (t < tags.size() && tags[t] != m->ev_tag[k]) ++t;
+    if (t == tags.size()) { tags.push_back(m->ev_tag[k]); tot.push_back(0); mn.push_back(1e30); mx.push_back(0); cnt.push_back(0); }
+    tot[t] += us; cnt[t] += 1;
+    if (us < mn[t]) mn[t] = us;
+    if (us > mx[t]) mx[t] = us;
+  }
+  std::string rep;
+  char line[256];
+  for (size_t t = 0; t < tags.size(); ++t) {
+    snprintf(line, sizeof line, "%s\t%lld\t%.3f\t%.3f\t%.3f\n", tags[t].c_str(), (long long)cnt[t], tot[t], mn[t], mx[t]);
+    rep += line;
+  }
+  if (out && out_len > 0) {
+    strncpy(out, rep.c_str(), (size_t)out_len - 1);
+    out[out_len - 1] = 0;
+  }
+  for (auto e : m->ev) (void)hipEventDestroy(e);
+  m->ev.clear();
+  m->ev_tag.clear();
+  m->ev_used = 0;
+  return P3D_OK;
+}

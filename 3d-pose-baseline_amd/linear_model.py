@@ -1,0 +1,489 @@
+"""MI355X-native drop-in for ``src/linear_model.py`` of EsauPR/3d-pose-baseline.
+
+``LinearModel`` keeps the reference constructor (src/linear_model.py:34-44), the
+``step`` feed/fetch API and return tuples (:203-245), ``get_all_batches``
+(:247-300) and the attributes its callers touch (``global_step``,
+``learning_rate``, ``saver``, ``train_writer``/``test_writer``, ``err_mm``,
+``err_mm_summary``, ``encoder_inputs``/``decoder_outputs``).  Underneath, every
+op of the TF1 graph runs in hand-written HIP kernels (libp3d.so, include/p3d.h):
+fused GEMM+bias+BN+ReLU+dropout layers on fp32 MFMA, a fused data-gradient +
+BN/ReLU/dropout backward, LDS-tiled weight gradients and a fused TF1 Adam.
+
+PyTorch-ROCm is used only as plumbing: device memory for I/O, the stream, and
+``torch.distributed`` (RCCL) for data-parallel training.  There is no CPU
+fallback: construction fails if libp3d.so cannot be loaded.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+
+import numpy as np
+
+import _p3d
+from _p3d import check, lib, ptr
+
+HUMAN_2D_SIZE = 16 * 2
+
+
+def kaiming(shape, rng: np.random.Generator):
+    """src/linear_model.py:17-29: truncated_normal(shape) * sqrt(2/shape[0]).
+
+    tf.truncated_normal re-draws samples beyond two standard deviations.
+    """
+    x = rng.standard_normal(shape)
+    bad = np.abs(x) > 2.0
+    while bad.any():
+        x[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(x) > 2.0
+    return (x * math.sqrt(2.0 / float(shape[0]))).astype(np.float32)
+
+
+def exponential_decay(lr0: float, global_step: int, decay_steps: int = 100000,
+                      decay_rate: float = 0.96) -> float:
+    """tf.train.exponential_decay, continuous (src/linear_model.py:88-90), in fp32."""
+    p = np.float32(global_step) / np.float32(decay_steps)
+    return float(np.float32(np.float32(lr0) * np.power(np.float32(decay_rate), p, dtype=np.float32)))
+
+
+class Summary:
+    """Stand-in for a serialized tf.Summary scalar (tag, value)."""
+
+    __slots__ = ("tag", "value")
+
+    def __init__(self, tag, value):
+        self.tag, self.value = tag, float(value)
+
+    def __repr__(self):
+        return "Summary(%s=%g)" % (self.tag, self.value)
+
+
+class SummaryWriter:
+    """tf.summary.FileWriter stand-in: appends JSON lines to <dir>/events.jsonl."""
+
+    def __init__(self, logdir):
+        self.logdir = logdir
+        self._path = None
+
+    def _file(self):
+        if self._path is None:
+            os.makedirs(self.logdir, exist_ok=True)
+            self._path = os.path.join(self.logdir, "events.jsonl")
+        return self._path
+
+    def add_summary(self, summary, global_step=None):
+        items = summary if isinstance(summary, (list, tuple)) else [summary]
+        with open(self._file(), "a") as f:
+            for s in items:
+                f.write(json.dumps({"step": None if global_step is None else int(global_step),
+                                    "tag": s.tag, "value": s.value, "wall": time.time()}) + "\n")
+
+    def add_graph(self, *_args, **_kw):
+        pass
+
+    def flush(self):
+        pass
+
+
+class _Scalar:
+    """Object with ``.eval()`` like the tf.Variable/Tensor the driver prints."""
+
+    def __init__(self, fn):
+        self._fn = fn
+
+    def eval(self, session=None):
+        return self._fn()
+
+
+class Placeholder:
+    def __init__(self, name, shape=None):
+        self.name, self.shape = name, shape
+
+
+class Saver:
+    """tf.train.Saver stand-in: every global variable (TF names), Adam slots and step
+    bookkeeping into ``<save_path>-<global_step>.npz``; keeps the last ``max_to_keep``."""
+
+    def __init__(self, model, max_to_keep=10):
+        self.model = model
+        self.max_to_keep = max_to_keep
+        self._saved = []
+
+    def save(self, session, save_path, global_step=None):
+        path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+        state = self.model.get_state()
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        np.savez(path + ".npz", **state)
+        with open(os.path.join(d or ".", "checkpoint"), "w") as f:
+            f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
+        self._saved.append(path)
+        while len(self._saved) > self.max_to_keep:
+            old = self._saved.pop(0)
+            if os.path.exists(old + ".npz"):
+                os.remove(old + ".npz")
+        return path
+
+    def restore(self, session, save_path):
+        p = save_path if save_path.endswith(".npz") else save_path + ".npz"
+        if not os.path.exists(p):
+            raise ValueError("Checkpoint %s does not seem to exist" % save_path)
+        with np.load(p, allow_pickle=False) as z:
+            self.model.set_state({k: z[k] for k in z.files})
+
+
+class LinearModel(object):
+    """A simple Linear+RELU model (src/linear_model.py:31), on MI355X HIP kernels."""
+
+    def __init__(self, linear_size, num_layers, residual, batch_norm, max_norm, batch_size,
+                 learning_rate, summaries_dir, predict_14=False, dtype=None, *, seed=None,
+                 max_batch=None, device=None, data_parallel=None, init=True):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise _p3d.P3DError("LinearModel needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                "the HIP path has no CPU fallback")
+        if dtype is not None and str(dtype).split(".")[-1] not in ("float32", "tf.float32"):
+            raise ValueError("this build implements the fp32 graph only (got dtype=%r)" % (dtype,))
+        self.torch = torch
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.HUMAN_2D_SIZE = HUMAN_2D_SIZE
+        self.HUMAN_3D_SIZE = 14 * 3 if predict_14 else 16 * 3
+        self.input_size = self.HUMAN_2D_SIZE
+        self.output_size = self.HUMAN_3D_SIZE
+        self.linear_size = int(linear_size)
+        self.num_layers = int(num_layers)
+        self.residual = bool(residual)
+        self.batch_norm = bool(batch_norm)
+        self.max_norm = bool(max_norm)
+        self.batch_size = int(batch_size)
+        self.predict_14 = bool(predict_14)
+        self.lr0 = float(learning_rate)
+        self.seed = int(seed if seed is not None else np.random.SeedSequence().entropy % (2 ** 63))
+        self.max_batch = int(max_batch or max(self.batch_size, 64))
+
+        cfg = _p3d.P3DCfg(self.linear_size, self.num_layers, int(self.residual), int(self.batch_norm),
+                          int(self.max_norm), self.input_size, self.output_size, _p3d.P3D_DTYPE_F32,
+                          self.max_batch, 1e-3, 0.99)
+        h = _p3d.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().p3d_create(_p3d.ctypes.byref(cfg), _p3d.ctypes.byref(h)), "p3d_create")
+        self._h = h
+        self._tables()
+
+        # placeholders / tensors the reference exposes (src/linear_model.py:77-134)
+        self.isTraining = Placeholder("isTrainingflag")
+        self.dropout_keep_prob = Placeholder("dropout_keep_prob")
+        self.encoder_inputs = Placeholder("inputs/enc_in", [None, self.input_size])
+        self.decoder_outputs = Placeholder("inputs/dec_out", [None, self.output_size])
+        self.err_mm = Placeholder("error_mm")
+        self.err_mm_summary = ("summary", "loss/error_mm")
+        self.outputs = "outputs"
+        self.train_writer = SummaryWriter(os.path.join(summaries_dir, "train"))
+        self.test_writer = SummaryWriter(os.path.join(summaries_dir, "test"))
+        self.global_step = _Scalar(lambda: self.get_step()[0])
+        self.learning_rate = _Scalar(lambda: exponential_decay(self.lr0, self.get_step()[0]))
+        self.saver = Saver(self, max_to_keep=10)
+
+        # data parallelism (pure DP over RCCL; see dist.py / DESIGN.md)
+        import torch.distributed as dist
+        if data_parallel is None:
+            data_parallel = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.data_parallel = bool(data_parallel)
+        self.rank = dist.get_rank() if self.data_parallel else 0
+        self.world = dist.get_world_size() if self.data_parallel else 1
+
+        self._loss_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._dy = torch.empty((self.max_batch, self.output_size), dtype=torch.float32, device=self.device)
+        if init:
+            self.initialize(self.seed)
+
+    # ------------------------------------------------------------------ plumbing
+    def _tables(self):
+        L = lib()
+        n = _p3d.c_int32()
+        check(L.p3d_param_count(self._h, _p3d.ctypes.byref(n)), "p3d_param_count")
+        self.param_table = []
+        for i in range(n.value):
+            name = _p3d.c_char_p()
+            numel = _p3d.c_int64()
+            kind = _p3d.c_int32()
+            off = _p3d.c_int64()
+            check(L.p3d_param_info(self._h, i, _p3d.ctypes.byref(name), _p3d.ctypes.byref(numel),
+                                   _p3d.ctypes.byref(kind), _p3d.ctypes.byref(off)), "p3d_param_info")
+            self.param_table.append((name.value.decode(), int(numel.value), int(kind.value), int(off.value)))
+        self.flat = {}
+        idx = self.device.index
+        for which, key in enumerate(("params", "grads", "adam_m", "adam_v", "moving")):
+            p = _p3d.c_void_p()
+            ne = _p3d.c_int64()
+            check(L.p3d_flat_ptr(self._h, which, _p3d.ctypes.byref(p), _p3d.ctypes.byref(ne)), "p3d_flat_ptr")
+            self.flat[key] = _p3d.device_view(p.value, (ne.value,), idx) if ne.value > 0 else None
+        self._shapes = {}
+        for name, numel, kind, off in self.param_table:
+            self._shapes[name] = self._shape_of(name, numel)
+
+    def _shape_of(self, name, numel):
+        base = name.split("/")[-1]
+        L = self.linear_size
+        if base == "w1":
+            return (self.input_size, L)
+        if base == "w4":
+            return (L, self.output_size)
+        if base.startswith("w2_") or base.startswith("w3_"):
+            return (L, L)
+        return (numel,)
+
+    def variable(self, name):
+        """Zero-copy torch view (device) of a TF-named variable."""
+        for n, numel, kind, off in self.param_table:
+            if n == name:
+                buf = self.flat["params"] if kind == 0 else self.flat["moving"]
+                return buf[off:off + numel].view(self._shapes[name])
+        raise KeyError(name)
+
+    def grad(self, name):
+        for n, numel, kind, off in self.param_table:
+            if n == name and kind == 0:
+                return self.flat["grads"][off:off + numel].view(self._shapes[name])
+        raise KeyError(name)
+
+    def trainable_names(self):
+        return [n for n, _, k, _ in self.param_table if k == 0]
+
+    def stream(self):
+        return _p3d.stream_handle()
+
+    def params_updated(self):
+        check(lib().p3d_params_updated(self._h, self.stream()), "p3d_params_updated")
+
+    def get_step(self):
+        gs = _p3d.c_int64()
+        b1 = _p3d.c_float()
+        b2 = _p3d.c_float()
+        check(lib().p3d_get_step(self._h, _p3d.ctypes.byref(gs), _p3d.ctypes.byref(b1),
+                                 _p3d.ctypes.byref(b2)), "p3d_get_step")
+        return int(gs.value), float(b1.value), float(b2.value)
+
+    # ------------------------------------------------------------------ init / state
+    def initialize(self, seed=None):
+        """tf.global_variables_initializer(): kaiming weights and biases, BN defaults,
+        zero Adam slots, global_step 0.  Rank 0's values are broadcast under DP."""
+        rng = np.random.default_rng(self.seed if seed is None else seed)
+        state = {}
+        for name, numel, kind, off in self.param_table:
+            if kind != 0:
+                continue
+            if name.endswith("/gamma"):
+                state[name] = np.ones(numel, np.float32)
+            elif name.endswith("/beta"):
+                state[name] = np.zeros(numel, np.float32)
+            else:
+                state[name] = kaiming(self._shapes[name], rng)
+        for name, numel, kind, off in self.param_table:
+            if kind == 1:
+                state[name] = (np.ones if name.endswith("moving_variance") else np.zeros)(numel, np.float32)
+        self.set_weights(state)
+        self.flat["adam_m"].zero_()
+        self.flat["adam_v"].zero_()
+        check(lib().p3d_set_step(self._h, 0, 0.9, 0.999), "p3d_set_step")
+        if self.data_parallel:
+            self.broadcast_parameters()
+
+    def set_weights(self, arrays: dict):
+        """Write TF-named arrays (any subset) into device memory, then refresh layouts."""
+        torch = self.torch
+        for name, val in arrays.items():
+            v = self.variable(name)
+            a = np.asarray(val, dtype=np.float32).reshape(v.shape)
+            v.copy_(torch.from_numpy(np.ascontiguousarray(a)))
+        self.params_updated()
+
+    def get_weights(self, include_moving=True):
+        out = {}
+        for name, numel, kind, off in self.param_table:
+            if kind == 0 or include_moving:
+                out[name] = self.variable(name).detach().cpu().numpy().copy()
+        return out
+
+    def get_state(self):
+        """Every global variable (tf.global_variables()) as numpy, TF names."""
+        st = self.get_weights(include_moving=True)
+        for name in self.trainable_names():
+            numel = self.variable(name).numel()
+            off = [o for n, _, k, o in self.param_table if n == name][0]
+            st[name + "/Adam"] = self.flat["adam_m"][off:off + numel].cpu().numpy().reshape(self._shapes[name])
+            st[name + "/Adam_1"] = self.flat["adam_v"][off:off + numel].cpu().numpy().reshape(self._shapes[name])
+        gs, b1, b2 = self.get_step()
+        st["global_step"] = np.array(gs, np.int64)
+        st["beta1_power"] = np.array(b1, np.float32)
+        st["beta2_power"] = np.array(b2, np.float32)
+        st["learning_rate"] = np.array(self.lr0, np.float32)
+        return st
+
+    def set_state(self, st):
+        torch = self.torch
+        self.set_weights({k: v for k, v in st.items() if k in self._shapes})
+        for name in self.trainable_names():
+            off = [o for n, _, k, o in self.param_table if n == name][0]
+            numel = self.variable(name).numel()
+            if name + "/Adam" in st:
+                self.flat["adam_m"][off:off + numel].copy_(torch.from_numpy(
+                    np.ascontiguousarray(st[name + "/Adam"], np.float32).reshape(-1)))
+                self.flat["adam_v"][off:off + numel].copy_(torch.from_numpy(
+                    np.ascontiguousarray(st[name + "/Adam_1"], np.float32).reshape(-1)))
+        if "global_step" in st:
+            check(lib().p3d_set_step(self._h, int(st["global_step"]), float(st["beta1_power"]),
+                                     float(st["beta2_power"])), "p3d_set_step")
+
+    def broadcast_parameters(self):
+        import torch.distributed as dist
+        for key in ("params", "moving", "adam_m", "adam_v"):
+            if self.flat[key] is not None:
+                dist.broadcast(self.flat[key], src=0)
+        self.params_updated()
+
+    # ------------------------------------------------------------------ device-side API
+    def _as_dev(self, a, width, what):
+        torch = self.torch
+        if isinstance(a, torch.Tensor):
+            t = a
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float32)))
+        if t.dim() != 2 or t.shape[1] != width:
+            raise ValueError("%s: expected shape [None, %d], got %s" % (what, width, tuple(t.shape)))
+        if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+            t = t.to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
+        return t
+
+    def forward_device(self, x, training=False, keep_prob=1.0, out=None, ctr=None):
+        """Device-resident forward: returns outputs [B, output_size] (no host sync)."""
+        x = self._as_dev(x, self.input_size, "enc_in")
+        B = x.shape[0]
+        if out is None:
+            out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
+        if ctr is None:
+            ctr = self.get_step()[0]
+        check(lib().p3d_forward(self._h, ptr(x), B, ptr(out), int(bool(training)), float(keep_prob),
+                                self.seed, int(ctr), self.rank * B, self.stream()), "p3d_forward")
+        return out
+
+    def loss_device(self, y, t, dy=None):
+        B = y.shape[0]
+        check(lib().p3d_mse(ptr(y), ptr(t), B, self.output_size, ptr(self._loss_dev),
+                            0 if dy is None else ptr(dy), self.stream()), "p3d_mse")
+        return self._loss_dev
+
+    def train_step_device(self, x, t, keep_prob, out=None):
+        """One TF1 training step (fwd + MSE + bwd + [all-reduce] + Adam), device resident.
+
+        Returns (loss_device_scalar, outputs).  Mirrors session.run([updates, loss, ...])
+        of src/linear_model.py:225-237.
+        """
+        x = self._as_dev(x, self.input_size, "enc_in")
+        t = self._as_dev(t, self.output_size, "dec_out")
+        B = x.shape[0]
+        if B > self.max_batch:
+            raise ValueError("batch %d exceeds max_batch %d" % (B, self.max_batch))
+        gs = self.get_step()[0]
+        self._x_keep = x  # the library differentiates this buffer in p3d_backward
+        y = self.forward_device(x, True, keep_prob, out=out, ctr=gs)
+        dy = self._dy[:B]
+        loss = self.loss_device(y, t, dy)
+        check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
+        if self.data_parallel:
+            self._allreduce_grads()
+        check(lib().p3d_adam_step(self._h, exponential_decay(self.lr0, gs), self.stream()), "p3d_adam_step")
+        return loss, y
+
+    def compute_gradients(self, x, t, keep_prob, ctr=None):
+        """Forward (training) + MSE + backward, no optimizer update (opt.compute_gradients,
+        src/linear_model.py:143).  Gradients land in ``self.flat['grads']`` / ``grad(name)``.
+        Note the training forward also applies the BN moving-average UPDATE_OPS."""
+        x = self._as_dev(x, self.input_size, "enc_in")
+        t = self._as_dev(t, self.output_size, "dec_out")
+        B = x.shape[0]
+        self._x_keep = x
+        y = self.forward_device(x, True, keep_prob, ctr=ctr)
+        dy = self._dy[:B]
+        loss = self.loss_device(y, t, dy)
+        check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
+        return loss, y
+
+    def _allreduce_grads(self):
+        import torch.distributed as dist
+        g = self.flat["grads"]
+        if dist.get_backend() == "nccl":
+            dist.all_reduce(g, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM)
+            g.div_(self.world)
+
+    # ------------------------------------------------------------------ reference API
+    def step(self, session, encoder_inputs, decoder_outputs, dropout_keep_prob, isTraining=True):
+        """src/linear_model.py:203-245.
+
+        Training: returns (loss, loss_summary, learning_rate_summary, outputs).
+        Eval:     returns (loss, loss_summary, outputs).
+        Inputs are numpy arrays (float64 is cast to float32 like the placeholders).
+        """
+        torch = self.torch
+        with torch.cuda.device(self.device):
+            if isTraining:
+                lr = exponential_decay(self.lr0, self.get_step()[0])
+                loss, y = self.train_step_device(encoder_inputs, decoder_outputs, dropout_keep_prob)
+                out = y.cpu().numpy()
+                lv = float(loss.item())
+                return lv, Summary("loss/loss", lv), Summary("learning_rate/learning_rate", lr), out
+            x = self._as_dev(encoder_inputs, self.input_size, "enc_in")
+            t = self._as_dev(decoder_outputs, self.output_size, "dec_out")
+            y = self.forward_device(x, False, float(dropout_keep_prob))
+            loss = self.loss_device(y, t)
+            out = y.cpu().numpy()
+            lv = float(loss.item())
+            return lv, Summary("loss/loss", lv), out
+
+    def get_all_batches(self, data_x, data_y, camera_frame, training=True):
+        """src/linear_model.py:247-300: concatenate in dict order, permute when training,
+        drop the ``n % batch_size`` tail, split into batches (float64 host arrays)."""
+        n = 0
+        for key2d in data_x.keys():
+            n += data_x[key2d].shape[0]
+        encoder_inputs = np.zeros((n, self.input_size), dtype=float)
+        decoder_outputs = np.zeros((n, self.output_size), dtype=float)
+        idx = 0
+        for key2d in data_x.keys():
+            (subj, b, fname) = key2d
+            key3d = key2d if camera_frame else (subj, b, '{0}.h5'.format(fname.split('.')[0]))
+            key3d = (subj, b, fname[:-3]) if fname.endswith('-sh') and camera_frame else key3d
+            n2d = data_x[key2d].shape[0]
+            encoder_inputs[idx:idx + n2d, :] = data_x[key2d]
+            decoder_outputs[idx:idx + n2d, :] = data_y[key3d]
+            idx += n2d
+        if training:
+            perm = np.random.permutation(n)
+            encoder_inputs = encoder_inputs[perm, :]
+            decoder_outputs = decoder_outputs[perm, :]
+        n_extra = n % self.batch_size
+        if n_extra > 0:
+            encoder_inputs = encoder_inputs[:-n_extra, :]
+            decoder_outputs = decoder_outputs[:-n_extra, :]
+        n_batches = n // self.batch_size
+        if n_batches == 0:
+            return [], []
+        return np.split(encoder_inputs, n_batches), np.split(decoder_outputs, n_batches)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.torch.cuda.synchronize(self.device)
+            lib().p3d_destroy(self._h)
+            self._h = _p3d.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

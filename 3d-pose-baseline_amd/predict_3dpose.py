@@ -1,0 +1,373 @@
+"""Driver / API of src/predict_3dpose.py on the MI355X-native model.
+
+Keeps: ``FLAGS`` (same flag names and defaults, src/predict_3dpose.py:31-107),
+the hyper-parameter-encoded ``train_dir`` (:110-123), ``create_model`` (:131-186),
+the epoch ``train`` loop (:188-334), ``get_action_subset`` (:337-349) and
+``evaluate_batches`` (:352-444).  Differences, all documented in DESIGN.md:
+
+* flags are parsed in ``main`` (the reference parses argv at import time); an
+  importable ``FLAGS`` object holds the defaults so front ends can import it;
+* the per-frame MPJPE (un-normalize, 17 joints, per-joint L2) runs on the GPU in
+  one fused kernel, accumulating fp64 per-joint sums on the device;
+* ``evaluate_action_wise`` shards each action's batches across the ranks of a
+  ``torch.distributed`` job and combines per-action sums with one RCCL
+  all-reduce;
+* the H3.6M loaders are not part of this build: ``--synthetic`` feeds data of
+  the reference's shapes.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+import _p3d
+import data_utils
+import linear_model
+from _p3d import check, lib, ptr
+
+
+def build_parser():
+    p = argparse.ArgumentParser()
+    p.add_argument("--learning_rate", type=float, default=1.0, help="Learning rate")
+    p.add_argument("--dropout", type=float, default=1, help="Dropout keep probability. 1 means no dropout")
+    p.add_argument("--batch_size", type=int, default=64, help="Batch size to use during training")
+    p.add_argument("--epochs", type=int, default=200, help="How many epochs we should train for")
+    p.add_argument("--camera_frame", action='store_true', default=False, help="Convert 3d poses to camera coordinates")
+    p.add_argument("--max_norm", action='store_true', default=False, help="Apply maxnorm constraint to the weights")
+    p.add_argument("--batch_norm", action='store_true', default=False, help="Use batch_normalization")
+    p.add_argument("--predict_14", action='store_true', default=False, help="predict 14 joints")
+    p.add_argument("--use_sh", action='store_true', default=False, help="Use 2d pose predictions from StackedHourglass")
+    p.add_argument("--action", type=str, default="All", help="The action to train on. 'All' means all the actions")
+    p.add_argument("--linear_size", type=int, default=1024, help="Size of each model layer.")
+    p.add_argument("--num_layers", type=int, default=2, help="Number of layers in the model.")
+    p.add_argument("--residual", action='store_true', default=False, help="Whether to add a residual connection every 2 layers")
+    p.add_argument("--procrustes", action='store_true', default=False, help="Apply procrustes analysis at test time")
+    p.add_argument("--evaluateActionWise", action='store_true', default=False, help="The dataset to use either h36m or heva")
+    p.add_argument("--cameras_path", type=str, default="data/h36m/cameras.h5", help="Directory to load camera parameters")
+    p.add_argument("--data_dir", type=str, default="data/h36m/", help="Data directory")
+    p.add_argument("--train_dir", type=str, default="experiments", help="Training directory.")
+    p.add_argument("--sample", action='store_true', default=False, help="Set to True for sampling.")
+    p.add_argument("--use_cpu", action='store_true', default=False, help="Whether to use the CPU")
+    p.add_argument("--load", type=int, default=0, help="Try to load a previous checkpoint.")
+    p.add_argument("--use_fp16", action='store_true', default=False, help="Train using fp16 instead of fp32.")
+    # build-specific
+    p.add_argument("--synthetic", action='store_true', default=False,
+                   help="Use synthetic H3.6M-shaped data (the dataset is not part of this build)")
+    p.add_argument("--seed", type=int, default=0, help="Weight / dropout seed")
+    return p
+
+
+FLAGS = build_parser().parse_args([])   # defaults; main() re-parses argv
+
+
+def train_dir_for(flags):
+    """Hyper-parameter-encoded train_dir (src/predict_3dpose.py:110-123)."""
+    return os.path.join(flags.train_dir, flags.action, 'dropout_{0}'.format(flags.dropout),
+                        'epochs_{0}'.format(flags.epochs) if flags.epochs > 0 else '',
+                        'lr_{0}'.format(flags.learning_rate),
+                        'residual' if flags.residual else 'not_residual',
+                        'depth_{0}'.format(flags.num_layers), 'linear_size{0}'.format(flags.linear_size),
+                        'batch_size_{0}'.format(flags.batch_size),
+                        'procrustes' if flags.procrustes else 'no_procrustes',
+                        'maxnorm' if flags.max_norm else 'no_maxnorm',
+                        'batch_normalization' if flags.batch_norm else 'no_batch_normalization',
+                        'use_stacked_hourglass' if flags.use_sh else 'not_stacked_hourglass',
+                        'predict_14' if flags.predict_14 else 'predict_17')
+
+
+class Session:
+    """Minimal stand-in for tf.Session: a context manager whose ``run`` evaluates the
+    few graph handles callers fetch outside ``step`` (err_mm_summary)."""
+
+    def __init__(self, *args, **kwargs):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+    def run(self, fetches, feed_dict=None):
+        feed_dict = feed_dict or {}
+        if isinstance(fetches, tuple) and fetches and fetches[0] == "summary":
+            val = next(iter(feed_dict.values()))
+            return linear_model.Summary(fetches[1], val)
+        if hasattr(fetches, "eval"):
+            return fetches.eval()
+        raise NotImplementedError("Session.run: unsupported fetch %r" % (fetches,))
+
+
+def create_model(session, actions, batch_size, flags=None):
+    """src/predict_3dpose.py:131-186: build the model, init fresh or restore --load."""
+    flags = flags or FLAGS
+    tdir = train_dir_for(flags)
+    if flags.use_fp16:
+        raise ValueError("--use_fp16 is not supported by this build (fp32 graph)")
+    model = linear_model.LinearModel(flags.linear_size, flags.num_layers, flags.residual, flags.batch_norm,
+                                     flags.max_norm, batch_size, flags.learning_rate,
+                                     os.path.join(tdir, "log"), flags.predict_14, seed=flags.seed,
+                                     max_batch=max(batch_size, 4096))
+    if flags.load <= 0:
+        print("Creating model with fresh parameters.")
+        return model
+    ck = os.path.join(tdir, "checkpoint-{0}".format(flags.load))
+    if not os.path.isfile(ck + ".npz"):
+        raise ValueError("Asked to load checkpoint {0}, but it does not seem to exist".format(flags.load))
+    print("Loading model {0}".format(ck))
+    model.saver.restore(session, ck)
+    return model
+
+
+def get_action_subset(poses_set, action):
+    """src/predict_3dpose.py:337-349."""
+    return {k: v for k, v in poses_set.items() if k[1] == action}
+
+
+class MPJPE:
+    """Device accumulator of per-joint L2 sums (p3d_mpjpe_accum), fp64."""
+
+    def __init__(self, model, data_mean_3d, data_std_3d, dim_to_use_3d, predict_14=False, procrustes=False):
+        import torch
+        if predict_14:
+            raise NotImplementedError("fused MPJPE implements the 17-joint protocol (predict_14 is not fused)")
+        if procrustes:
+            raise NotImplementedError("--procrustes (Protocol #2) is not fused in this build")
+        self.torch = torch
+        self.model = model
+        dev = model.device
+        self.mean = torch.as_tensor(np.asarray(data_mean_3d, np.float64), device=dev)
+        self.std = torch.as_tensor(np.asarray(data_std_3d, np.float64), device=dev)
+        self.dims = torch.as_tensor(np.asarray(dim_to_use_3d, np.int32), device=dev)
+        if self.mean.numel() != 96 or self.std.numel() != 96 or self.dims.numel() != 48:
+            raise ValueError("MPJPE expects 96-d mean/std and 48 used dims")
+        self.joint_sum = torch.zeros(17, dtype=torch.float64, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.frames = 0
+        self.batches = 0
+
+    def add(self, pred, gt, loss=None, nbatches=1):
+        B = pred.shape[0]
+        check(lib().p3d_mpjpe_accum(ptr(pred), ptr(gt), ptr(self.mean), ptr(self.std), ptr(self.dims), B,
+                                    ptr(self.joint_sum), self.model.stream()), "p3d_mpjpe_accum")
+        if loss is not None:
+            self.loss_sum += loss.double() * nbatches
+        self.frames += B
+        self.batches += nbatches
+
+
+def _stack(batches, width):
+    if len(batches) == 0:
+        return np.zeros((0, width), np.float32)
+    return np.ascontiguousarray(np.vstack(batches), dtype=np.float32)
+
+
+def run_eval_rows(model, acc, X, Y, batch_size, chunk_rows=4096):
+    """Forward + fused MPJPE over whole batches of device rows X/Y (no host sync).
+
+    Inference rows are independent (BN uses moving statistics), so consecutive
+    batches are submitted together in chunks of up to ``chunk_rows``.
+    """
+    n = X.shape[0]
+    chunk = max(batch_size, (min(chunk_rows, model.max_batch) // batch_size) * batch_size)
+    out = model.torch.empty((min(chunk, max(n, 1)), model.output_size), dtype=model.torch.float32,
+                            device=model.device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        y = model.forward_device(X[s:e], False, 1.0, out=out[:e - s])
+        loss = model.loss_device(y, Y[s:e])
+        acc.add(y, Y[s:e], loss, (e - s) // batch_size)
+
+
+def evaluate_batches(sess, model, data_mean_3d, data_std_3d, dim_to_use_3d, dim_to_ignore_3d,
+                     data_mean_2d, data_std_2d, dim_to_use_2d, dim_to_ignore_2d,
+                     current_step, encoder_inputs, decoder_outputs, current_epoch=0, flags=None):
+    """src/predict_3dpose.py:352-444 -> (total_err, joint_err, step_time, loss)."""
+    flags = flags or FLAGS
+    torch = model.torch
+    nbatches = len(encoder_inputs)
+    for b in encoder_inputs:
+        if b.shape[0] != model.batch_size:
+            raise AssertionError("batch of %d != batch_size %d" % (b.shape[0], model.batch_size))
+    start = time.time()
+    acc = MPJPE(model, data_mean_3d, data_std_3d, dim_to_use_3d, flags.predict_14, flags.procrustes)
+    with torch.cuda.device(model.device):
+        X = torch.from_numpy(_stack(encoder_inputs, model.input_size)).to(model.device)
+        Y = torch.from_numpy(_stack(decoder_outputs, model.output_size)).to(model.device)
+        run_eval_rows(model, acc, X, Y, model.batch_size)
+        js = acc.joint_sum.cpu().numpy()
+        loss = float(acc.loss_sum.item())
+    step_time = (time.time() - start) / max(nbatches, 1)
+    n = max(acc.frames, 1)
+    joint_err = js / n
+    total_err = float(np.sum(js) / (n * 17))
+    return total_err, joint_err, step_time, loss / max(nbatches, 1)
+
+
+def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std_3d, dim_to_use_3d,
+                         actions, camera_frame=True, flags=None):
+    """Per-action MPJPE sweep (src/predict_3dpose.py:274-298), frame-sharded.
+
+    Each action's batch list (after the reference's per-action n % B tail drop) is
+    split contiguously across the ranks of the current torch.distributed job; every
+    rank accumulates fp64 per-joint sums, frame counts and loss sums on its GPU and
+    one all-reduce over a [n_actions, 19] fp64 tensor combines them.  Returns
+    ({action: mm}, average_mm) with the reference's unweighted Average.
+    """
+    import torch
+    import torch.distributed as dist
+    flags = flags or FLAGS
+    dist_on = dist.is_available() and dist.is_initialized()
+    rank = dist.get_rank() if dist_on else 0
+    world = dist.get_world_size() if dist_on else 1
+    table = torch.zeros((len(actions), 19), dtype=torch.float64, device=model.device)
+    with torch.cuda.device(model.device):
+        for ai, action in enumerate(actions):
+            enc, dec = model.get_all_batches(get_action_subset(test_set_2d, action),
+                                             get_action_subset(test_set_3d, action), camera_frame,
+                                             training=False)
+            nb = len(enc)
+            lo, hi = (nb * rank) // world, (nb * (rank + 1)) // world
+            acc = MPJPE(model, data_mean_3d, data_std_3d, dim_to_use_3d, flags.predict_14, flags.procrustes)
+            if hi > lo:
+                X = torch.from_numpy(_stack(enc[lo:hi], model.input_size)).to(model.device)
+                Y = torch.from_numpy(_stack(dec[lo:hi], model.output_size)).to(model.device)
+                run_eval_rows(model, acc, X, Y, model.batch_size)
+            table[ai, :17] = acc.joint_sum
+            table[ai, 17] = float(acc.frames)
+            table[ai, 18] = acc.loss_sum[0]
+        if dist_on and world > 1:
+            dist.all_reduce(table, op=dist.ReduceOp.SUM)
+        t = table.cpu().numpy()
+    errs = {}
+    for ai, action in enumerate(actions):
+        n = max(t[ai, 17], 1.0)
+        errs[action] = float(np.sum(t[ai, :17]) / (n * 17))
+    return errs, float(np.mean([errs[a] for a in actions]))
+
+
+def synthetic_h36m(n_train=20000, n_test=4000, seed=0, out_dim=48):
+    """Normalized H3.6M-shaped data (keys (subject, action, seqname)) and stats."""
+    rng = np.random.default_rng(seed)
+    actions = data_utils.define_actions("All")
+    use3, ign3 = data_utils.dimension_sets(3)
+    use2, ign2 = data_utils.dimension_sets(2)
+    mean3 = np.zeros(96)
+    std3 = np.zeros(96)
+    mean3[use3] = rng.uniform(-500, 500, len(use3))
+    std3[use3] = rng.uniform(50, 300, len(use3))
+    mean2 = np.zeros(64)
+    std2 = np.ones(64)
+    mean2[use2] = rng.uniform(200, 800, len(use2))
+    std2[use2] = rng.uniform(20, 120, len(use2))
+    proj = rng.standard_normal((32, out_dim)) / np.sqrt(32)
+
+    def make(subjects, n):
+        s2, s3 = {}, {}
+        for a in actions:
+            for j, subj in enumerate(subjects):
+                k = max(1, n // (len(actions) * len(subjects)))
+                x = rng.standard_normal((k + j * 7, 32))
+                s2[(subj, a, "%s.%d.h5" % (a, j))] = x
+                s3[(subj, a, "%s.%d.h5" % (a, j))] = np.tanh(x @ proj) + 0.1 * rng.standard_normal((len(x), out_dim))
+        return s2, s3
+
+    tr2, tr3 = make(data_utils.TRAIN_SUBJECTS, n_train)
+    te2, te3 = make(data_utils.TEST_SUBJECTS, n_test)
+    return dict(train_set_2d=tr2, train_set_3d=tr3, test_set_2d=te2, test_set_3d=te3, data_mean_3d=mean3,
+                data_std_3d=std3, dim_to_use_3d=use3, dim_to_ignore_3d=ign3, data_mean_2d=mean2,
+                data_std_2d=std2, dim_to_use_2d=use2, dim_to_ignore_2d=ign2)
+
+
+def load_data(flags):
+    if flags.synthetic:
+        return synthetic_h36m(out_dim=42 if flags.predict_14 else 48, seed=flags.seed)
+    raise NotImplementedError("H3.6M loaders (read_3d_data / read_2d_predictions) are not part of this "
+                              "build; pass --synthetic or feed normalized arrays to LinearModel.step")
+
+
+def train(flags=None):
+    """Epoch loop of src/predict_3dpose.py:188-334 on the MI355X model."""
+    flags = flags or FLAGS
+    actions = data_utils.define_actions(flags.action)
+    d = load_data(flags)
+    tdir = train_dir_for(flags)
+    os.makedirs(os.path.join(tdir, "log"), exist_ok=True)
+    with Session() as sess:
+        print("Creating %d bi-layers of %d units." % (flags.num_layers, flags.linear_size))
+        model = create_model(sess, actions, flags.batch_size, flags)
+        print("Model created")
+        current_step = 0 if flags.load <= 0 else flags.load + 1
+        log_every_n_batches = 100
+        for epoch in range(1, flags.epochs + 1):
+            enc, dec = model.get_all_batches(d["train_set_2d"], d["train_set_3d"], flags.camera_frame,
+                                             training=True)
+            nbatches = len(enc)
+            print("There are {0} train batches".format(nbatches))
+            start_time, loss = time.time(), 0.
+            for i in range(nbatches):
+                step_loss, loss_summary, lr_summary, _ = model.step(sess, enc[i], dec[i], flags.dropout,
+                                                                    isTraining=True)
+                if (i + 1) % log_every_n_batches == 0:
+                    model.train_writer.add_summary(loss_summary, current_step)
+                    model.train_writer.add_summary(lr_summary, current_step)
+                    step_time = time.time() - start_time
+                    start_time = time.time()
+                    print("Working on epoch {0}, batch {1} / {2}... done in {3:.2f} ms".format(
+                        epoch, i + 1, nbatches, 1000 * step_time / log_every_n_batches))
+                loss += step_loss
+                current_step += 1
+            loss = loss / max(nbatches, 1)
+            print("=============================\n"
+                  "Global step:         %d\n"
+                  "Learning rate:       %.2e\n"
+                  "Train loss avg:      %.4f\n"
+                  "=============================" % (model.global_step.eval(), model.learning_rate.eval(), loss))
+            if flags.evaluateActionWise:
+                print("{0:=^12} {1:=^6}".format("Action", "mm"))
+                errs, avg = evaluate_action_wise(model, d["test_set_2d"], d["test_set_3d"], d["data_mean_3d"],
+                                                 d["data_std_3d"], d["dim_to_use_3d"], actions,
+                                                 flags.camera_frame, flags)
+                for a in actions:
+                    print("{0:<12} {1:>6.2f}".format(a, errs[a]))
+                model.test_writer.add_summary(sess.run(model.err_mm_summary, {model.err_mm: avg}), current_step)
+                print("{0:<12} {1:>6.2f}".format("Average", avg))
+                print("{0:=^19}".format(''))
+            else:
+                enc, dec = model.get_all_batches(d["test_set_2d"], d["test_set_3d"], flags.camera_frame,
+                                                 training=False)
+                total_err, joint_err, step_time, vloss = evaluate_batches(
+                    sess, model, d["data_mean_3d"], d["data_std_3d"], d["dim_to_use_3d"], d["dim_to_ignore_3d"],
+                    d["data_mean_2d"], d["data_std_2d"], d["dim_to_use_2d"], d["dim_to_ignore_2d"],
+                    current_step, enc, dec, epoch, flags)
+                print("=============================\n"
+                      "Step-time (ms):      %.4f\n"
+                      "Val loss avg:        %.4f\n"
+                      "Val error avg (mm):  %.2f\n"
+                      "=============================" % (1000 * step_time, vloss, total_err))
+                for i in range(17 if not flags.predict_14 else 14):
+                    print("Error in joint {0:02d} (mm): {1:>5.2f}".format(i + 1, joint_err[i]))
+                model.test_writer.add_summary(sess.run(model.err_mm_summary, {model.err_mm: total_err}),
+                                              current_step)
+            print("Saving the model... ", end="")
+            t0 = time.time()
+            model.saver.save(sess, os.path.join(tdir, 'checkpoint'), global_step=current_step)
+            print("done in {0:.2f} ms".format(1000 * (time.time() - t0)))
+            sys.stdout.flush()
+    return model
+
+
+def main(argv=None):
+    global FLAGS
+    FLAGS = build_parser().parse_args(argv)
+    if FLAGS.sample:
+        raise NotImplementedError("sample() is matplotlib visualisation (out of scope for this build)")
+    return train(FLAGS)
+
+
+if __name__ == "__main__":
+    main()

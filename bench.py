@@ -1,0 +1,254 @@
+"""Benchmark of the MI355X pose-lifting MLP (BASELINE.json metric: poses/s at batch 64).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode infer|train|eval]
+
+Modes (BASELINE.json configs):
+  infer  (default, configs[1]) L=1024, 2 residual blocks, BN, batch 64, fp32 inference.
+         One step = one forward pass over one batch of 64 poses (its own synthetic
+         batch, resident in HBM).  Steps are issued back to back on one stream and
+         replayed from a HIP graph of G steps (launch overhead amortised; every step
+         still runs its own six layer kernels over its own 64 rows).
+  train  (configs[2]) same model, one step = fwd + MSE + bwd + [RCCL all-reduce] +
+         TF1 Adam at batch 64 per GPU, keep_prob 0.5.
+  eval   (configs[3]) evaluateActionWise sweep over a synthetic 15-action H3.6M-shaped
+         test set, batches sharded across ranks, one all-reduce of per-action sums.
+
+Multi-GPU: one process per GPU (torch.distributed.run); inference shards by batch
+with no data-path collective (scaling "weak"); train is data parallel (RCCL).
+Rank 0 prints ONE JSON line.  Alongside `value` it reports `roofline` (dominant
+kernel timed live with hipEvent pairs, see p3d_profile_*) and `cpu_baseline`
+(the numpy fp32 restatement of the TF1 path, oracle/ref_mlp.py, on the host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+sys.path.insert(0, ROOT)
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+
+L, NBLK, IN, OUT, BATCH = 1024, 2, 32, 48, 64
+
+
+def flops_per_pose(L=L, N=NBLK):
+    """2*(32L + 2N*L^2 + 48L) GEMM FLOP per pose (forward)."""
+    return 2 * (IN * L + 2 * N * L * L + OUT * L)
+
+
+def setup_dist():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier_sync(world):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_model(seed=1234, max_batch=BATCH, data_parallel=None):
+    """Kaiming weights (LinearModel.initialize) + non-trivial BN statistics."""
+    import linear_model
+    m = linear_model.LinearModel(L, NBLK, True, True, False, BATCH, 1e-3, "/tmp/p3d_bench", seed=seed,
+                                 max_batch=max_batch, data_parallel=data_parallel)
+    rng = np.random.default_rng(2)
+    bn = {}
+    for name, numel, kind, _ in m.param_table:
+        if name.endswith("/gamma"):
+            bn[name] = rng.uniform(0.5, 1.5, numel)
+        elif name.endswith("/beta") or name.endswith("/moving_mean"):
+            bn[name] = rng.normal(0.0, 0.1, numel)
+        elif name.endswith("/moving_variance"):
+            bn[name] = rng.uniform(0.5, 2.0, numel)
+    m.set_weights(bn)
+    return m, None
+
+
+def profile_kernels(model, fn, n_launch_max=4096):
+    """Run fn() with every model kernel bracketed by hipEvent pairs -> {tag: (count, avg_us)}."""
+    import ctypes
+    import _p3d
+    _p3d.check(_p3d.lib().p3d_profile_start(model._h, n_launch_max), "p3d_profile_start")
+    fn()
+    buf = ctypes.create_string_buffer(1 << 16)
+    _p3d.check(_p3d.lib().p3d_profile_stop(model._h, buf, len(buf)), "p3d_profile_stop")
+    out = {}
+    for line in buf.value.decode().strip().splitlines():
+        tag, cnt, tot, mn, mx = line.split("\t")
+        out[tag] = (int(cnt), float(tot) / int(cnt), float(mn), float(mx))
+    return out
+
+
+def cpu_baseline(mode, seconds=12.0):
+    """numpy fp32 restatement of the TF1 path (oracle/ref_mlp.py) on this host's cores."""
+    from oracle import ref_mlp
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = 1
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=NBLK, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((BATCH, IN)).astype(np.float32)
+    t = rng.standard_normal((BATCH, OUT)).astype(np.float32)
+    fn = (lambda: ref_mlp.eval_step(st, x, t, dt=np.float32)) if mode != "train" else \
+        (lambda: ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=1, dt=np.float32))
+    for _ in range(3):
+        fn()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * BATCH / dt, 1), "unit": "poses/s", "cores": int(threads), "kind": "port",
+            "sample": "%d %s batches of 64 (cfg2 model, fp32 numpy restatement of src/linear_model.py), %.1f s"
+                      % (n, "train-step" if mode == "train" else "inference", dt)}
+
+
+def bench_infer(args, rank, world):
+    import torch
+    model, _ = make_model(data_parallel=False)
+    G = args.graph_steps
+    while args.steps % G:
+        G -= 1
+    rng = np.random.default_rng(100 + rank)
+    X = torch.from_numpy(rng.standard_normal((G, BATCH, IN)).astype(np.float32)).cuda()
+    Y = torch.empty((G, BATCH, OUT), dtype=torch.float32, device="cuda")
+
+    def steps_eager(k):
+        for i in range(k):
+            model.forward_device(X[i % G], False, 1.0, out=Y[i % G], ctr=0)
+
+    # capture G steps (each its own batch) into one HIP graph
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        steps_eager(G)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        steps_eager(G)
+    reps_w = max(1, args.warmup // G)
+    for _ in range(reps_w):
+        graph.replay()
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps // G):
+        graph.replay()
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    value = world * args.steps * BATCH / dt
+
+    # live per-kernel timing of the same steps (eager, event pair per launch)
+    prof = profile_kernels(model, lambda: steps_eager(min(args.steps, 200)))
+    cnt, avg_us, _, _ = prof["fwd_hidden"]
+    flop = 2.0 * BATCH * L * L          # one hidden-layer launch: [64,1024] x [1024,1024]
+    achieved = flop / (avg_us * 1e-6) / 1e12
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": args.traffic,
+            "kernel": "k_fwd<1,4,8,1> (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
+            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": cnt,
+            "per_kernel_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+    model.close()
+    return value, dt, roof
+
+
+def bench_train(args, rank, world):
+    import torch
+    model, _ = make_model(data_parallel=world > 1)
+    rng = np.random.default_rng(200 + rank)
+    G = 16
+    X = torch.from_numpy(rng.standard_normal((G, BATCH, IN)).astype(np.float32)).cuda()
+    T = torch.from_numpy(rng.standard_normal((G, BATCH, OUT)).astype(np.float32)).cuda()
+    Y = torch.empty((BATCH, OUT), dtype=torch.float32, device="cuda")
+
+    def run(k):
+        for i in range(k):
+            model.train_step_device(X[i % G], T[i % G], 0.5, out=Y)
+
+    run(args.warmup)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    run(args.steps)
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    value = world * args.steps * BATCH / dt
+    prof = profile_kernels(model, lambda: run(min(args.steps, 50)))
+    # dominant = Adam over the 4,291,632 trainables: p,m,v read+write, g read = 7 x 4 B
+    n_params = sum(n for _, n, k, _ in model.param_table if k == 0)
+    cnt, avg_us, _, _ = prof["adam"]
+    byts = 7 * 4 * n_params
+    achieved = byts / (avg_us * 1e-6) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": args.traffic, "kernel": "k_adam",
+            "bytes_per_launch": byts, "avg_us": round(avg_us, 3),
+            "per_kernel_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+    model.close()
+    return value, dt, roof
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--mode", choices=["infer", "train"], default="infer")
+    ap.add_argument("--graph-steps", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", type=float, default=None,
+                    help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
+    args = ap.parse_args()
+    rank, world, local = setup_dist()
+    if args.gpus != world and world > 1:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if args.mode == "infer":
+        value, dt, roof = bench_infer(args, rank, world)
+        workload = "cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step"
+    else:
+        value, dt, roof = bench_train(args, rank, world)
+        workload = "cfg3 train step: L=1024, 2 residual blocks, BN, dropout keep 0.5, batch 64/GPU, TF1 Adam"
+    if rank == 0:
+        cpu = None if args.no_cpu else cpu_baseline(args.mode, args.cpu_seconds)
+        line = {"metric": "poses/sec at batch 64 (H3.6M 16-joint)", "value": round(value, 1), "unit": "poses/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(1000.0 * dt / args.steps, 5), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": workload, "global_batch": BATCH * world, "linear_size": L,
+                           "num_layers": NBLK, "parallelism": "dp%d" % world},
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

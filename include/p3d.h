@@ -1,0 +1,136 @@
+/*
+ * p3d.h -- C ABI of the MI355X-native 2D->3D pose-lifting MLP (libp3d.so).
+ *
+ * This is the drop-in boundary for the hot path of EsauPR/3d-pose-baseline:
+ * the TF1 graph of src/linear_model.py (LinearModel.__init__ :34-151,
+ * two_linear :154-201, step :203-245) and the MPJPE arithmetic of
+ * src/predict_3dpose.py:evaluate_batches (:352-444).  The reference has no
+ * FFI of its own (it is 100% Python over TensorFlow); each entry point below
+ * replaces the TensorFlow op group named in its comment, and the Python host
+ * (3d-pose-baseline_amd/linear_model.py) binds them through ctypes exactly as
+ * INTEGRATION.md shows.
+ *
+ * Conventions
+ *   - Plain C: int status return (P3D_OK = 0), message via p3d_last_error().
+ *   - The library owns parameters, optimizer slots and workspace (device memory).
+ *     The caller owns every I/O buffer passed in; all I/O pointers are DEVICE
+ *     pointers, row-major, fp32 unless stated.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *     Every call is asynchronous on that stream.
+ *   - One model handle per stream/thread; calls on one handle are not thread-safe.
+ */
+#ifndef P3D_H_
+#define P3D_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P3D_OK 0
+#define P3D_ERR_ARG 1      /* bad argument / shape (TF: InvalidArgumentError) */
+#define P3D_ERR_HIP 2      /* HIP runtime failure                            */
+#define P3D_ERR_STATE 3    /* call out of order (e.g. backward before fwd)   */
+#define P3D_ERR_NOTFOUND 4 /* unknown parameter name                         */
+
+#define P3D_DTYPE_F32 0
+#define P3D_DTYPE_BF16 1   /* bf16 weights/activations, fp32 accumulate + BN */
+
+typedef struct p3d_cfg {
+  int32_t linear_size;  /* LinearModel(linear_size)            linear_model.py:35 */
+  int32_t num_layers;   /* number of two_linear blocks          linear_model.py:36 */
+  int32_t residual;     /* two_linear residual add              linear_model.py:199 */
+  int32_t batch_norm;   /* tf.layers.batch_normalization        linear_model.py:112 */
+  int32_t max_norm;     /* tf.clip_by_norm(w, 1)                linear_model.py:108 */
+  int32_t input_size;   /* HUMAN_2D_SIZE = 32                   linear_model.py:62  */
+  int32_t output_size;  /* HUMAN_3D_SIZE = 48 (42 if predict_14) linear_model.py:72 */
+  int32_t dtype;        /* P3D_DTYPE_*                                              */
+  int32_t max_batch;    /* largest B any call will use (workspace sizing)           */
+  float bn_eps;         /* 1e-3 (TF default)                                        */
+  float bn_momentum;    /* 0.99 (TF default)                                        */
+} p3d_cfg;
+
+typedef struct p3d_model p3d_model;
+
+/* Last error message of the calling thread ("" if none). */
+const char* p3d_last_error(void);
+
+/* Build a model: allocates trainables (TF creation order), BN moving stats,
+ * Adam slots, gradients and activation workspace.  Replaces the variable
+ * creation + tf.global_variables_initializer of linear_model.py:84-151
+ * (values are zero/one; the host writes kaiming weights via p3d_param_ptr). */
+int p3d_create(const p3d_cfg* cfg, p3d_model** out);
+int p3d_destroy(p3d_model* m);
+
+/* Parameter table.  Names are TF1 variable names, e.g. "linear_model/w1",
+ * "linear_model/two_linear_0/batch_normalization10/moving_mean".  Weights are
+ * stored [in, out] row-major exactly like the TF variables (linear_model.py:103).
+ * kind: 0 = trainable, 1 = BN moving statistic.  Indexing is 0..count-1. */
+int p3d_param_count(const p3d_model* m, int32_t* count);
+int p3d_param_info(const p3d_model* m, int32_t idx, const char** name, int64_t* numel,
+                   int32_t* kind, int64_t* offset);
+int p3d_param_ptr(p3d_model* m, const char* name, void** dptr, int64_t* numel);
+
+/* Flat device buffers (trainables in TF order, 256-byte aligned segments):
+ * params/grads/adam_m/adam_v share one layout; `numel` is the padded length.
+ * grads is what data-parallel training all-reduces. */
+int p3d_flat_ptr(p3d_model* m, int32_t which /*0 params,1 grads,2 adam_m,3 adam_v,4 moving*/,
+                 void** dptr, int64_t* numel);
+
+/* Must be called after the host writes parameters through p3d_param_ptr /
+ * p3d_flat_ptr (refreshes derived device layouts, e.g. transposed weights). */
+int p3d_params_updated(p3d_model* m, void* stream);
+
+/* Forward pass: y[B, output_size] = MLP(x[B, input_size]).
+ *   training=0: BN uses moving statistics (isTraining=False, linear_model.py:239-245)
+ *   training=1: BN uses batch statistics, updates the moving averages
+ *               (UPDATE_OPS, linear_model.py:138-140) and caches activations
+ *               for p3d_backward.  Requires B <= max_batch.
+ *   keep_prob:  tf.nn.dropout keep probability (1 = identity); the mask is
+ *               Philox4x32-10 keyed by (seed, ctr, site, row_offset + row, col).
+ * Replaces the forward ops of linear_model.py:103-128. */
+int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
+                float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, void* stream);
+
+/* MSE loss of linear_model.py:129 and its gradient: loss = mean((y-t)^2) over
+ * B*D, dy = (1/(B*D)) * 2*(y-t).  loss_dev: one device float (may be NULL),
+ * dy may be NULL. */
+int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, float* loss_dev, float* dy,
+            void* stream);
+
+/* Backward pass of the last training forward: gradients of every trainable
+ * into the flat grads buffer (opt.compute_gradients, linear_model.py:143). */
+int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stream);
+
+/* One TF1 ApplyAdam over all trainables (linear_model.py:137,145):
+ *   alpha = lr*sqrt(1-beta2_power)/(1-beta1_power); m += (g-m)(1-b1);
+ *   v += (g^2-v)(1-b2); w -= (m*alpha)/(sqrt(v)+eps)
+ * lr is the already-decayed rate (tf.train.exponential_decay is host-side:
+ * lr0 * 0.96^(global_step/1e5)).  beta powers advance and global_step += 1. */
+int p3d_adam_step(p3d_model* m, float lr, void* stream);
+
+/* Adam bookkeeping (for checkpoints): global_step and beta1/beta2 powers. */
+int p3d_get_step(const p3d_model* m, int64_t* global_step, float* beta1_power, float* beta2_power);
+int p3d_set_step(p3d_model* m, int64_t global_step, float beta1_power, float beta2_power);
+
+/* Fused MPJPE accumulation of src/predict_3dpose.py:399-430 for one batch:
+ *   pred_n [B, 48] fp32 network outputs, gt_n [B, 48] fp32 normalized targets,
+ *   mean96/std96 [96] fp64 (data_mean_3d / data_std_3d), dims48 [48] int32
+ *   (dim_to_use_3d).  Un-normalizes both (x*std+mean, fp64, root dims = mean),
+ *   takes the 17 joints [0,1,2] + dims48, and ADDS per-joint L2 sums (fp64) into
+ *   joint_sum17[17].  Procrustes is not fused here. */
+int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96,
+                    const double* std96, const int32_t* dims48, int64_t B, double* joint_sum17,
+                    void* stream);
+
+/* Live kernel timing (bench.py's roofline): while active, every kernel the model
+ * launches is bracketed by a hipEvent pair.  p3d_profile_stop synchronises and writes
+ * one line per kernel tag: "tag\tcount\ttotal_us\tmin_us\tmax_us\n". */
+int p3d_profile_start(p3d_model* m, int32_t max_launches);
+int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P3D_H_ */

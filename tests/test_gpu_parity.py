@@ -1,0 +1,171 @@
+"""HIP path vs the CPU oracle (oracle/ref_mlp.py, oracle/ref_eval.py) on the GPU.
+
+Tolerances (fp32 path vs fp64 oracle):
+* outputs: |d| <= 2e-5 + 2e-5*|ref| (fp32 MFMA contraction over K<=1024 is an
+  exact fp32 fmaf chain; the oracle accumulates in fp64);
+* MPJPE: |d| <= 1e-4 mm (north_star);
+* gradients / Adam updates: relative 1e-3 of each tensor's max magnitude;
+  pre-BN biases are excluded from post-Adam comparisons: their gradient is
+  analytically zero under batch-norm and Adam normalises its rounding noise
+  ("pre-BN bias").
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import linear_model  # noqa: E402
+import predict_3dpose  # noqa: E402
+from oracle import ref_eval, ref_mlp  # noqa: E402
+
+
+def make(cfg, seed=1, bn_seed=2, batch=64, max_batch=None, lr=1e-3, model_seed=11):
+    st = ref_mlp.init_state(cfg, seed=seed, bn_seed=bn_seed)
+    m = linear_model.LinearModel(cfg.linear_size, cfg.num_layers, cfg.residual, cfg.batch_norm, cfg.max_norm,
+                                 batch, lr, "/tmp/p3d_test", cfg.predict_14, seed=model_seed,
+                                 max_batch=max_batch or max(batch, 64))
+    m.set_weights({**st.params, **st.moving})
+    return st, m
+
+
+def close(a, b, atol=2e-5, rtol=2e-5):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    err = np.abs(a - b)
+    tol = atol + rtol * np.abs(b)
+    assert np.all(err <= tol), "max err %.3g (at ref %.3g)" % (err.max(), b.flat[np.argmax(err - tol)])
+
+
+@pytest.mark.parametrize("L,N,B", [(256, 1, 64), (1024, 2, 64), (1024, 2, 1), (1024, 2, 37), (256, 3, 200)])
+def test_eval_forward(L, N, B):
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
+    st, m = make(cfg, batch=B, max_batch=max(B, 64))
+    rng = np.random.default_rng(B)
+    x = rng.standard_normal((B, 32))
+    t = rng.standard_normal((B, 48))
+    loss, _, out = m.step(None, x, t, 1.0, isTraining=False)
+    rl, ro = ref_mlp.eval_step(st, x, t)
+    close(out, ro)
+    assert abs(loss - rl) <= 1e-5 * max(1.0, abs(rl))
+    m.close()
+
+
+@pytest.mark.parametrize("residual,batch_norm,max_norm", [(False, False, False), (True, False, False),
+                                                          (False, True, False), (True, True, True)])
+def test_eval_variants(residual, batch_norm, max_norm):
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=residual, batch_norm=batch_norm, max_norm=max_norm)
+    st, m = make(cfg)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((64, 32))
+    t = rng.standard_normal((64, 48))
+    _, _, out = m.step(None, x, t, 1.0, isTraining=False)
+    _, ro = ref_mlp.eval_step(st, x, t)
+    close(out, ro, atol=5e-5, rtol=5e-5)
+    m.close()
+
+
+def _grad_check(cfg, keep, B=64):
+    st, m = make(cfg, batch=B)
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((B, 32))
+    t = rng.standard_normal((B, 48))
+    loss, y = m.compute_gradients(x, t, keep, ctr=3)
+    out, cache = ref_mlp.forward(st, x, True, keep, m.seed, 3, 0)
+    rl, dy = ref_mlp.mse(out, t)
+    grads = ref_mlp.backward(st, cache, dy)
+    close(y.cpu().numpy(), out, atol=5e-5, rtol=5e-5)
+    assert abs(float(loss.item()) - rl) <= 1e-5 * max(1.0, rl)
+    for name in m.trainable_names():
+        g = m.grad(name).cpu().numpy()
+        r = grads[name]
+        scale = max(np.abs(r).max(), 1e-30)
+        if cfg.batch_norm and ("/b1" in name or "/b2_" in name or "/b3_" in name):
+            # analytically zero under BN: only check it is noise-sized
+            assert np.abs(g).max() < 1e-4, name
+            continue
+        err = np.abs(g - r).max() / scale
+        assert err < 1e-3, "%s rel err %.3g" % (name, err)
+    # BN moving statistics (UPDATE_OPS) after one training forward
+    ref_mlp.bn_update(st, cache)
+    for k, v in st.moving.items():
+        close(m.variable(k).cpu().numpy(), v, atol=2e-5, rtol=2e-5)
+    m.close()
+
+
+@pytest.mark.parametrize("keep", [1.0, 0.5])
+def test_gradients_cfg2(keep):
+    _grad_check(ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True), keep)
+
+
+@pytest.mark.parametrize("residual,batch_norm,max_norm,B", [(False, False, False, 64), (True, False, False, 32),
+                                                            (False, True, False, 64), (True, True, True, 64),
+                                                            (True, True, False, 17)])
+def test_gradients_variants(residual, batch_norm, max_norm, B):
+    _grad_check(ref_mlp.Cfg(linear_size=256, num_layers=2, residual=residual, batch_norm=batch_norm,
+                            max_norm=max_norm), 0.5, B)
+
+
+def test_train_steps_track_oracle():
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg, lr=1e-3)
+    rng = np.random.default_rng(21)
+    for step in range(5):
+        x = rng.standard_normal((64, 32))
+        t = rng.standard_normal((64, 48))
+        loss, _, lr_sum, out = m.step(None, x, t, 0.5, isTraining=True)
+        rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
+        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=1e-3, rtol=1e-3)
+    gs, b1, b2 = m.get_step()
+    assert gs == 5 and abs(b1 - 0.9 ** 6) < 1e-6 and abs(b2 - 0.999 ** 6) < 1e-6
+    w = m.get_weights()
+    for name in m.trainable_names():
+        if "/b1" in name or "/b2_" in name or "/b3_" in name:
+            continue
+        err = np.abs(w[name] - st.params[name]).max()
+        assert err < 5e-5, (name, err)
+    m.close()
+
+
+def test_mpjpe_kernel_matches_reference_goldens():
+    g = np.load("tests/golden/reference_goldens.npz", allow_pickle=False)
+    st, m = make(ref_mlp.Cfg(linear_size=256, num_layers=1))
+    acc = predict_3dpose.MPJPE(m, g["nd_mean"], g["nd_std"], g["ns_use3"])
+    pred = torch.from_numpy(g["mp_pred_n"]).cuda()
+    gt = torch.from_numpy(g["mp_gt_n"].astype(np.float32)).cuda()
+    acc.add(pred, gt)
+    js = acc.joint_sum.cpu().numpy()
+    ref = g["mp_dists"].sum(axis=0)
+    np.testing.assert_allclose(js, ref, rtol=1e-12, atol=1e-9)
+    m.close()
+
+
+def test_mpjpe_end_to_end_within_1e4_mm():
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    stats = ref_eval.synthetic_stats()
+    s2, s3 = ref_eval.synthetic_test_set(scale=0.02)
+    enc, dec = m.get_all_batches(s2, s3, True, training=False)
+    err, jerr, _, loss = predict_3dpose.evaluate_batches(
+        None, m, stats["mean3"], stats["std3"], stats["use3"], stats["ign3"], stats["mean2"], stats["std2"],
+        stats["use2"], stats["ign2"], 0, enc, dec)
+    r_err, r_jerr, r_loss = ref_eval.evaluate_batches(lambda e, d: ref_mlp.eval_step(st, e, d), enc, dec,
+                                                      stats["mean3"], stats["std3"], stats["use3"], stats["ign3"])
+    assert abs(err - r_err) <= 1e-4, (err, r_err)
+    np.testing.assert_allclose(jerr, r_jerr, atol=1e-4)
+    assert abs(loss - r_loss) <= 1e-5 * max(1, r_loss)
+    m.close()
+
+
+def test_bad_shapes_raise():
+    st, m = make(ref_mlp.Cfg(linear_size=256, num_layers=1))
+    with pytest.raises(ValueError):
+        m.step(None, np.zeros((4, 31)), np.zeros((4, 48)), 1.0, isTraining=False)
+    with pytest.raises(ValueError):
+        m.step(None, np.zeros((4, 32)), np.zeros((4, 47)), 1.0, isTraining=False)
+    with pytest.raises(ValueError):
+        m.forward_device(torch.zeros((4096, 32), device="cuda"))
+    m.close()
