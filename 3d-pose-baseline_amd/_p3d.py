@@ -42,6 +42,8 @@ SIGNATURES = [
     ("p3d_params_updated", c_int32, [c_void_p, c_void_p]),
     ("p3d_forward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,
                               c_uint64, c_int64, c_void_p]),
+    ("p3d_forward_ex", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,
+                                 c_uint64, c_int64, c_int64, c_void_p]),
     ("p3d_mse", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_backward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_adam_step", c_int32, [c_void_p, c_float, c_void_p]),

@@ -2,17 +2,17 @@
 // pose-lifting MLP: the hot path of EsauPR/3d-pose-baseline src/linear_model.py.
 //
 // Kernels (one launch each, all on the caller's stream):
-//   k_fwd<RS,WK>      Y = epi(X*W + b): fp32 MFMA NT-GEMM + fused epilogue
-//                     (max-norm scale, bias, BN eval|train (+moving-average update),
-//                      ReLU, Philox dropout, residual add).  linear_model.py:103-124,171-199
-//   k_dgrad<WK>       dX = dZ*W^T (+ residual grad) fused with the PREVIOUS layer's
-//                     dropout/ReLU/BN backward -> dZ_prev, dgamma, dbeta.
-//   k_wgrad           dW = X^T*dZ and db = colsum(dZ) (64x64 output tiles, LDS staged).
-//   k_adam            TF1 ApplyAdam over the flat trainable buffer.   linear_model.py:137,145
-//   k_transpose       refresh Wt = W^T after a parameter change.
-//   k_mse             loss = mean((y-t)^2), dy = 2(y-t)/(B*D).          linear_model.py:129
-//   k_mpjpe           fused un-normalize + per-joint L2 (fp64).        predict_3dpose.py:399-430
-//   k_dot_*           per-tensor reductions for --max_norm (||W||^2, <G,W>).
+//   k_fwd        Y = epi(X*W + b): fp32 MFMA GEMM on fragment-major operands + fused
+//                epilogue (max-norm scale, bias, BN eval|train (+moving-average update),
+//                ReLU, Philox dropout, residual add).     linear_model.py:103-124,171-199
+//   k_dgrad      dX = dZ*W^T (+ residual grad) fused with the PREVIOUS layer's
+//                dropout/ReLU/BN backward -> dZ_prev, dgamma, dbeta.
+//   k_wgrad      dW = X^T*dZ and db = colsum(dZ) (64x64 tiles, LDS staged).
+//   k_adam       TF1 ApplyAdam over the flat trainable buffer.  linear_model.py:137,145
+//   k_pack       W (TF layout) -> the two fragment-major operand copies Wf / Wd.
+//   k_mse        loss = mean((y-t)^2), dy = 2(y-t)/(B*D).     linear_model.py:129
+//   k_mpjpe      fused un-normalize + per-joint L2 (fp64).   predict_3dpose.py:399-430
+//   k_dot_*      per-tensor reductions for --max_norm (||W||^2, <G,W>).
 #include "p3d_kernels.h"
 #include "../../include/p3d.h"
 
@@ -27,8 +27,8 @@
 // forward
 // =====================================================================================
 struct FwdArgs {
-  const float* X; int64_t ldx;    // [M, K]
-  const float* Wt; int64_t ldw;   // [N, K]  (transposed weight)
+  const float* X; int64_t ldx;    // [M, K]: packed (ldx unused) or row-major (input layer)
+  const float* Wf;                // packed forward weight, ngB = K/16 groups per column tile
   const float* bias;              // [N]
   const float* wsq;               // max-norm: ||W||^2 (device scalar) or null
   int M, K, N;
@@ -36,55 +36,59 @@ struct FwdArgs {
   const float* gamma; const float* beta;
   float* mmean; float* mvar;      // moving stats (read in eval, updated in train)
   float eps; float decay;         // decay = 1 - momentum (fp32, as TF computes it)
-  float* z_save;                  // train: z = X*W + b  [M, N]
+  float* z_save;                  // train: z = X*W + b, packed [M, N]
   float* mean_save; float* var_save;
   int relu;
   float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
-  const float* res; int64_t ldr;  // residual added after dropout
-  float* Y; int64_t ldy;
+  const float* res;               // residual added after dropout, packed [M, N]
+  float* Y; int64_t ldy;          // packed (hidden) or row-major (output layer)
 };
 
-// KIND only separates the symbols of the input / hidden / output layers so that
-// rocprof attributes their (very different) durations separately.
-template <int RS, int WK, int DEPTH, int KIND>
+// RS row tiles of 16 per wave; WK waves split the contraction; KIND only separates the
+// symbols of the input / hidden / output layers for rocprof.
+template <int RS, int WK, int DEPTH, int NACC, bool APK, bool YPK, int KIND>
 __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16 * RS;
-  const int ngt = p.K >> 4;
-  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
-  f32x4 acc[RS];
-#pragma unroll
-  for (int s = 0; s < RS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  p3d_nt_core<RS, DEPTH>(p.X, p.ldx, p.M, m0, p.Wt, p.ldw, p.N, n0, gb, ge, acc);
-  if (WK > 1) {
-    if (w > 0) {
-#pragma unroll
-      for (int s = 0; s < RS; ++s) red[((w - 1) * RS + s) * 64 + lane] = acc[s];
-    }
-    __syncthreads();
-    if (w > 0) return;
-#pragma unroll
-    for (int u = 1; u < WK; ++u)
-#pragma unroll
-      for (int s = 0; s < RS; ++s) acc[s] += red[((u - 1) * RS + s) * 64 + lane];
-  }
-  // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r, column n0+i -------------------
   const int i = lane & 15, q = lane >> 4;
+  const int ct = blockIdx.x, n0 = ct * 16, m0 = blockIdx.y * 16 * RS;
   const int col = n0 + i;
   const bool cok = col < p.N;
   const int cc = cok ? col : p.N - 1;
+  const int ngN = (p.N + 15) >> 4;
+  // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
+  float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
+  if (w == 0) {
+    b = p.bias[cc];
+    if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 16 * s + 4 * q + r;
+        rv[s][r] = p.res ? p.res[p3d_pk(row, cc, ngN)] : 0.f;
+      }
+  }
+  const int ngt = p.K >> 4;
+  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
+  f32x4 acc[NACC][RS];
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_core<RS, DEPTH, NACC, APK>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
+  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
+  // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r of column n0+i ---------------
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
-  const float b = p.bias[cc];
   float z[RS][4];
 #pragma unroll
   for (int s = 0; s < RS; ++s)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) z[s][r] = (p.wsq ? acc[s][r] / mx : acc[s][r]) + b;
+    for (int r = 0; r < 4; ++r) z[s][r] = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + b;
 
   float inv = 1.0f, shift = 0.0f;
   if (p.bn) {
-    float mean, var;
+    float mean = mmu, var = mva;
     if (p.bn == 2) {  // batch statistics over all M rows (host guarantees M <= 16*RS)
       float sum = 0.f;
 #pragma unroll
@@ -105,16 +109,12 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       if (q == 0 && cok) {
         p.mean_save[col] = mean;
         p.var_save[col] = var;
-        const float mm = p.mmean[col], mv = p.mvar[col];
-        p.mmean[col] = mm - (mm - mean) * p.decay;
-        p.mvar[col] = mv - (mv - var) * p.decay;
+        p.mmean[col] = mmu - (mmu - mean) * p.decay;
+        p.mvar[col] = mva - (mva - var) * p.decay;
       }
-    } else {
-      mean = p.mmean[cc];
-      var = p.mvar[cc];
     }
-    inv = (1.0f / sqrtf(var + p.eps)) * p.gamma[cc];
-    shift = p.beta[cc] - mean * inv;
+    inv = (1.0f / sqrtf(var + p.eps)) * gam;
+    shift = bet - mean * inv;
   }
   if (!cok) return;
 #pragma unroll
@@ -123,64 +123,71 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
-      if (p.z_save) p.z_save[(int64_t)row * p.N + col] = z[s][r];
+      if (p.z_save) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
       float y = p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
       if (p.keep < 1.0f) {
         const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + row, col);
         y = (y / p.keep) * p3d_dropout_mask(p.keep, u);
       }
-      if (p.res) y += p.res[(int64_t)row * p.ldr + col];
-      p.Y[(int64_t)row * p.ldy + col] = y;
+      if (p.res) y += rv[s][r];
+      if (YPK) p.Y[p3d_pk(row, col, ngN)] = y;
+      else p.Y[(int64_t)row * p.ldy + col] = y;
     }
 }
 
 // =====================================================================================
-// data gradient + previous layer's epilogue backward
+// data gradient + previous layer's epilogue backward (whole batch per workgroup)
 // =====================================================================================
 struct BwdArgs {
-  const float* dZ; int64_t ldz;   // A  = dZ [M, N]
-  const float* W; int64_t ldw;    // Bt = W  [K, N] (TF layout)
+  const float* dZ; int64_t ldz;   // A = dZ [M, N]: packed, or row-major (dy of the output layer)
+  const float* Wd;                // packed dgrad weight: rows = K (in), cols = N padded (ngB groups)
+  int ngB;
   const float* wsq;
   int M, K, N;                    // output [M, K]
-  const float* dres; int64_t ldres;  // residual gradient added to dX (block output grad)
-  float* draw; int64_t ldraw;     // store dX (+dres) if non-null
+  const float* dres;              // residual gradient added to dX (block output grad), packed [M,K]
+  float* draw;                    // store dX (+dres) packed if non-null
   int prev;                       // 1: run prev layer's dropout/relu/BN backward
-  int bn; const float* z; const float* mean; const float* var;
+  int bn; const float* z; const float* mean; const float* var;   // prev layer: z packed [M,K]
   const float* gamma; const float* beta; float eps;
   int relu; float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
-  float* dz; int64_t lddz;        // [M, K] gradient wrt prev layer's z
+  float* dz;                      // packed [M, K]: gradient wrt prev layer's z
   float* dgamma; float* dbeta;    // [K]
 };
 
-template <int WK, int DEPTH, int KIND>
+template <int WK, int DEPTH, int NACC, bool APK, int KIND>
 __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   constexpr int RS = 4;
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
-  const int ngt = p.N >> 4;
-  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
-  f32x4 acc[RS];
-#pragma unroll
-  for (int s = 0; s < RS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  p3d_nt_core<RS, DEPTH>(p.dZ, p.ldz, p.M, 0, p.W, p.ldw, p.K, n0, gb, ge, acc);
-  if (WK > 1) {
-    if (w > 0) {
-#pragma unroll
-      for (int s = 0; s < RS; ++s) red[((w - 1) * RS + s) * 64 + lane] = acc[s];
-    }
-    __syncthreads();
-    if (w > 0) return;
-#pragma unroll
-    for (int u = 1; u < WK; ++u)
-#pragma unroll
-      for (int s = 0; s < RS; ++s) acc[s] += red[((u - 1) * RS + s) * 64 + lane];
-  }
   const int i = lane & 15, q = lane >> 4;
+  const int ct = blockIdx.x, n0 = ct * 16;
   const int col = n0 + i;
   const bool cok = col < p.K;
   const int cc = cok ? col : p.K - 1;
+  const int ngK = p.K >> 4;
+  // prefetch the epilogue's per-column and per-element operands
+  float mean = 0.f, var = 1.f, gam = 1.f, bet = 0.f, zz[RS][4], dr[RS][4];
+  if (w == 0) {
+    if (p.prev && p.bn) { mean = p.mean[cc]; var = p.var[cc]; gam = p.gamma[cc]; bet = p.beta[cc]; }
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * s + 4 * q + r;
+        zz[s][r] = p.prev ? p.z[p3d_pk(row, cc, ngK)] : 0.f;
+        dr[s][r] = p.dres ? p.dres[p3d_pk(row, cc, ngK)] : 0.f;
+      }
+  }
+  const int ngt = p.ngB;
+  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
+  f32x4 acc[NACC][RS];
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, 0, p.Wd, ngt, ct, gb, ge, acc);
+  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
   float g[RS][4];
 #pragma unroll
@@ -188,20 +195,17 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * s + 4 * q + r;
-      const int rr = row < p.M ? row : p.M - 1;
-      float d = p.wsq ? acc[s][r] / mx : acc[s][r];
-      if (p.dres) d += p.dres[(int64_t)rr * p.ldres + cc];
-      if (p.draw && cok && row < p.M) p.draw[(int64_t)row * p.ldraw + col] = d;
+      const float d = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + dr[s][r];
+      if (p.draw && cok && row < p.M) p.draw[p3d_pk(row, col, ngK)] = d;
       g[s][r] = d;
     }
   if (!p.prev) return;
   // previous layer: y = dropout(relu(BN(z))) ; recompute a = BN(z) for the relu mask
-  float mean = 0.f, rstd = 1.f, inv = 1.f, shift = 0.f;
+  float rstd = 1.f, inv = 1.f, shift = 0.f;
   if (p.bn) {
-    mean = p.mean[cc];
-    rstd = 1.0f / sqrtf(p.var[cc] + p.eps);
-    inv = rstd * p.gamma[cc];
-    shift = p.beta[cc] - mean * inv;
+    rstd = 1.0f / sqrtf(var + p.eps);
+    inv = rstd * gam;
+    shift = bet - mean * inv;
   }
   float xh[RS][4];
   float sg = 0.f, sgx = 0.f;
@@ -211,18 +215,16 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * s + 4 * q + r;
       const bool ok = row < p.M;
-      const int rr = ok ? row : p.M - 1;
-      const float zz = p.z[(int64_t)rr * p.K + cc];
       float gg = g[s][r];
       if (p.keep < 1.0f) {
-        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + rr, cc);
+        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + row, cc);
         gg = (gg * p3d_dropout_mask(p.keep, u)) / p.keep;
       }
-      const float a = p.bn ? zz * inv + shift : zz;
+      const float a = p.bn ? zz[s][r] * inv + shift : zz[s][r];
       if (p.relu && !(a > 0.0f)) gg = 0.0f;
       if (!ok) gg = 0.0f;
       g[s][r] = gg;
-      const float x = (zz - mean) * rstd;
+      const float x = (zz[s][r] - mean) * rstd;
       xh[s][r] = x;
       sg += gg;
       sgx += gg * x;
@@ -241,24 +243,50 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
       const int row = 16 * s + 4 * q + r;
       if (row >= p.M) continue;
       const float dz = p.bn ? (inv / fm) * (fm * g[s][r] - sg - xh[s][r] * sgx) : g[s][r];
-      p.dz[(int64_t)row * p.lddz + col] = dz;
+      p.dz[p3d_pk(row, col, ngK)] = dz;
     }
 }
 
 // =====================================================================================
 // weight gradient: dW[K,N] = X^T[K,M] * dZ[M,N];  db[N] = colsum(dZ)
 // 64x64 output tile per 256-thread workgroup; wave w owns k-rows [16w,16w+16) and the
-// four 16-column subtiles.  Batch (contraction) staged through LDS in chunks of 64.
+// four 16-column subtiles.  The batch (contraction) is staged through LDS in chunks of 64.
 // =====================================================================================
 struct WgradArgs {
-  const float* X; int64_t ldx;    // [M, K]
-  const float* dZ; int64_t ldz;   // [M, N]
+  const float* X; int64_t ldx; int xpk;   // [M, K] packed (xpk) or row-major
+  const float* dZ; int64_t ldz; int zpk;  // [M, N] packed (zpk) or row-major
   int M, K, N;
-  float* dW;                      // [K, N]
+  float* dW;                      // [K, N] (TF layout, into the flat grads buffer)
   float* db;                      // [N] or null
 };
 
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
+
+// Stage rows [mc, mc+64) x cols [c0, c0+64) of a packed or row-major [R, C] source.
+__device__ __forceinline__ void p3d_stage64(float* __restrict__ dst, const float* __restrict__ src, int pk, int64_t ld,
+                                            int R, int C, int mc, int c0) {
+  const int tid = threadIdx.x;
+  if (pk) {  // 16 packed 1 KB tiles (4 row tiles x 4 column groups); C is a multiple of 16
+    const int ng = C >> 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e, chunk = idx >> 6, ln = idx & 63;
+      const int rt = chunk >> 2, gg = chunk & 3;
+      const int row = 16 * rt + (ln & 15), col = 16 * gg + 4 * (ln >> 4);
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mc + row < R && c0 + 16 * gg < C)
+        v = ((const f32x4*)src)[((int64_t)((mc >> 4) + rt) * ng + (c0 >> 4) + gg) * 64 + ln];
+      *(f32x4*)&dst[row * WG_LDS_STRIDE + col] = v;
+    }
+  } else {
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int m = e >> 6, c = e & 63;
+      float v = 0.f;
+      if (mc + m < R && c0 + c < C) v = src[(int64_t)(mc + m) * ld + c0 + c];
+      dst[m * WG_LDS_STRIDE + c] = v;
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[64 * WG_LDS_STRIDE];
@@ -271,18 +299,8 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
   for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
   for (int mc = 0; mc < p.M; mc += 64) {
-    // stage X[mc..mc+64)[k0..k0+64) and dZ[mc..mc+64)[n0..n0+64)
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int m = e >> 6, c = e & 63;
-      const int gm = mc + m;
-      float xv = 0.f, zv = 0.f;
-      if (gm < p.M) {
-        if (k0 + c < p.K) xv = p.X[(int64_t)gm * p.ldx + k0 + c];
-        if (n0 + c < p.N) zv = p.dZ[(int64_t)gm * p.ldz + n0 + c];
-      }
-      xs[m * WG_LDS_STRIDE + c] = xv;
-      zs[m * WG_LDS_STRIDE + c] = zv;
-    }
+    p3d_stage64(xs, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
+    p3d_stage64(zs, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
     __syncthreads();
 #pragma unroll 4
     for (int t = 0; t < 16; ++t) {
@@ -335,36 +353,44 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ w, float* __re
 }
 
 // =====================================================================================
-// transpose W [R, C] -> Wt [C, R] for every weight tensor (one launch)
+// pack every weight W [K, N] into Wf (rows n, cols k) and Wd (rows k, cols n padded)
 // =====================================================================================
 #define P3D_MAX_W 40
-struct TransTable {
+struct PackTable {
   int n;
-  int rows[P3D_MAX_W], cols[P3D_MAX_W];
-  int tile_begin[P3D_MAX_W + 1];
-  int64_t src[P3D_MAX_W], dst[P3D_MAX_W];  // element offsets into params / wt buffers
+  int K[P3D_MAX_W], N[P3D_MAX_W];
+  int64_t src[P3D_MAX_W], dstf[P3D_MAX_W], dstd[P3D_MAX_W];  // element offsets
+  int64_t begin[P3D_MAX_W + 1];  // float4 prefix over (Wf + Wd) outputs
 };
 
-__global__ __launch_bounds__(256) void k_transpose(const float* __restrict__ params, float* __restrict__ wt,
-                                                   TransTable tt) {
-  __shared__ float tile[32][33];
+__global__ __launch_bounds__(256) void k_pack(const float* __restrict__ params, float* __restrict__ wpk, PackTable pt) {
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= pt.begin[pt.n]) return;
   int t = 0;
-  while (t + 1 < tt.n && (int)blockIdx.x >= tt.tile_begin[t + 1]) ++t;
-  const int R = tt.rows[t], C = tt.cols[t];
-  const int local = blockIdx.x - tt.tile_begin[t];
-  const int tc = (C + 31) / 32;
-  const int r0 = (local / tc) * 32, c0 = (local % tc) * 32;
-  const float* src = params + tt.src[t];
-  float* dst = wt + tt.dst[t];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  for (int y = ty; y < 32; y += 8) {
-    const int r = r0 + y, c = c0 + tx;
-    tile[y][tx] = (r < R && c < C) ? src[(int64_t)r * C + c] : 0.f;
-  }
-  __syncthreads();
-  for (int y = ty; y < 32; y += 8) {
-    const int c = c0 + y, r = r0 + tx;
-    if (c < C && r < R) dst[(int64_t)c * R + r] = tile[tx][y];
+  while (t + 1 < pt.n && o >= pt.begin[t + 1]) ++t;
+  const int K = pt.K[t], N = pt.N[t], NP = (N + 15) & ~15;
+  const float* W = params + pt.src[t];
+  const int64_t local = o - pt.begin[t];
+  const int64_t nf = (int64_t)NP * K / 4;   // float4s in Wf
+  const bool isf = local < nf;
+  const int64_t li = isf ? local : local - nf;
+  const int64_t chunk = li >> 6;
+  const int ln = (int)(li & 63);
+  f32x4 v;
+  if (isf) {  // rows n (NP), cols k (K): chunk = ct * (K/16) + g
+    const int ngc = K >> 4;
+    const int ctile = (int)(chunk / ngc), g = (int)(chunk % ngc);
+    const int n = 16 * ctile + (ln & 15), k = 16 * g + 4 * (ln >> 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = n < N ? W[(int64_t)(k + e) * N + n] : 0.f;
+    ((f32x4*)(wpk + pt.dstf[t]))[li] = v;
+  } else {    // rows k (K), cols n (NP): chunk = kt * (NP/16) + g
+    const int ngc = NP >> 4;
+    const int kt = (int)(chunk / ngc), g = (int)(chunk % ngc);
+    const int k = 16 * kt + (ln & 15), n = 16 * g + 4 * (ln >> 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (n + e) < N ? W[(int64_t)k * N + n + e] : 0.f;
+    ((f32x4*)(wpk + pt.dstd[t]))[li] = v;
   }
 }
 
@@ -513,7 +539,7 @@ struct Layer {
   int K, N;
   int64_t w, b, gamma = -1, beta = -1;  // offsets in params
   int64_t mmean = -1, mvar = -1;        // offsets in moving
-  int64_t wt;                           // offset in wt buffer
+  int64_t wf, wd;                       // offsets in the packed-weight buffer
   int widx;                             // weight index (max-norm tables)
   int site;                             // dropout site; -1 for the output layer
   bool bn, relu;
@@ -525,19 +551,19 @@ struct p3d_model {
   p3d_cfg cfg;
   std::vector<Tensor> tensors;
   std::vector<Layer> layers;  // in, A0, B0, ..., out
-  int64_t n_flat = 0, n_moving = 0, n_wt = 0;
+  int64_t n_flat = 0, n_moving = 0, n_wpk = 0;
+  int64_t Bpad = 0;           // max_batch rounded up to 64 (packed row padding)
   float* flat[4] = {nullptr, nullptr, nullptr, nullptr};  // params, grads, m, v
   float* moving = nullptr;
-  float* wt = nullptr;
+  float* wpk = nullptr;       // packed weights (Wf, Wd per layer)
   float* ws = nullptr;        // activation workspace
-  int64_t ws_elems = 0;
   float* scratch = nullptr;   // reductions (max-norm)
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
-  TransTable tt;
+  PackTable pt;
   DotTable wtab;
-  // per-layer workspace pointers (B_max rows)
-  std::vector<float*> act;    // output of layer l (block layer B_i holds the block output)
+  // per-layer workspace (packed, Bpad rows)
+  std::vector<float*> act;    // output of layer l (layer B_i holds the block output)
   std::vector<float*> z;      // pre-BN z of layer l
   std::vector<float*> bmean, bvar;
   std::vector<float*> dz;     // gradient wrt z of layer l
@@ -572,17 +598,24 @@ struct ProfScope {  // brackets one kernel launch with an event pair when profil
     if (on) { (void)hipEventRecord(m->ev[2 * m->ev_used + 1], st); ++m->ev_used; }
   }
 };
+
+void free_all(p3d_model* m) {
+  for (auto e : m->ev) (void)hipEventDestroy(e);
+  for (auto& p : m->flat) if (p) (void)hipFree(p);
+  if (m->moving) (void)hipFree(m->moving);
+  if (m->wpk) (void)hipFree(m->wpk);
+  if (m->ws) (void)hipFree(m->ws);
+  if (m->scratch) (void)hipFree(m->scratch);
+}
 }  // namespace
 
 extern "C" const char* p3d_last_error(void) { return g_err.c_str(); }
 
-static int layer_count(const p3d_cfg& c) { return 2 + 2 * c.num_layers; }
-
 extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (!cfg_in || !out) return fail(P3D_ERR_ARG, "p3d_create: null argument");
   const p3d_cfg c = *cfg_in;
-  if (c.linear_size <= 0 || c.linear_size % 16 != 0)
-    return fail(P3D_ERR_ARG, "linear_size must be a positive multiple of 16");
+  if (c.linear_size <= 0 || c.linear_size % 64 != 0)
+    return fail(P3D_ERR_ARG, "linear_size must be a positive multiple of 64");
   if (c.num_layers < 0) return fail(P3D_ERR_ARG, "num_layers must be >= 0");
   if (c.input_size <= 0 || c.input_size % 16 != 0)
     return fail(P3D_ERR_ARG, "input_size must be a positive multiple of 16");
@@ -592,8 +625,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   p3d_model* m = new p3d_model();
   m->cfg = c;
   const int L = c.linear_size;
-  const int OUTP = (c.output_size + 15) / 16 * 16;  // padded output features (Wt rows)
-  (void)OUTP;
+  m->Bpad = pad64(c.max_batch);
   auto add = [&](const std::string& name, int64_t n) {
     Tensor t{name, n, m->n_flat, 0};
     m->n_flat += pad64(n);
@@ -641,43 +673,37 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   lo.w = add("linear_model/w4", (int64_t)L * c.output_size);
   lo.b = add("linear_model/b4", c.output_size);
   m->layers.push_back(lo);
-  // moving statistics (non-trainable)
   if (c.batch_norm) {
     for (size_t l = 0; l + 1 < m->layers.size(); ++l) {
       m->layers[l].mmean = addm(bn_scope[l] + "/moving_mean", L);
       m->layers[l].mvar = addm(bn_scope[l] + "/moving_variance", L);
     }
   }
-  // transposed-weight buffer and tables
-  m->tt.n = 0;
+  // packed-weight buffer and tables
+  m->pt.n = 0;
   m->wtab.n = 0;
-  int tiles = 0;
+  int64_t f4 = 0;
   for (size_t l = 0; l < m->layers.size(); ++l) {
     Layer& ly = m->layers[l];
-    const int K = ly.K, N = ly.N;
-    ly.wt = m->n_wt;
-    const int NP = (N + 15) / 16 * 16;
-    m->n_wt += pad64((int64_t)NP * K);
-    const int t = m->tt.n++;
+    const int K = ly.K, N = ly.N, NP = (N + 15) / 16 * 16;
+    const int t = m->pt.n++;
     if (t >= P3D_MAX_W) { delete m; return fail(P3D_ERR_ARG, "too many layers"); }
-    m->tt.rows[t] = K; m->tt.cols[t] = N;
-    m->tt.src[t] = ly.w; m->tt.dst[t] = ly.wt;
-    m->tt.tile_begin[t] = tiles;
-    tiles += ((K + 31) / 32) * ((N + 31) / 32);
+    ly.wf = m->n_wpk; m->n_wpk += pad64((int64_t)NP * K);
+    ly.wd = m->n_wpk; m->n_wpk += pad64((int64_t)NP * K);
+    m->pt.K[t] = K; m->pt.N[t] = N;
+    m->pt.src[t] = ly.w; m->pt.dstf[t] = ly.wf; m->pt.dstd[t] = ly.wd;
+    m->pt.begin[t] = f4;
+    f4 += 2 * (int64_t)NP * K / 4;
     ly.widx = t;
     m->wtab.off[t] = ly.w;
     m->wtab.len[t] = (int64_t)K * N;
     m->wtab.n = t + 1;
   }
-  m->tt.tile_begin[m->tt.n] = tiles;
+  m->pt.begin[m->pt.n] = f4;
 
   auto cleanup = [&](hipError_t e) {
     g_err = std::string("p3d_create: ") + hipGetErrorString(e);
-    for (auto& p : m->flat) if (p) (void)hipFree(p);
-    if (m->moving) (void)hipFree(m->moving);
-    if (m->wt) (void)hipFree(m->wt);
-    if (m->ws) (void)hipFree(m->ws);
-    if (m->scratch) (void)hipFree(m->scratch);
+    free_all(m);
     delete m;
     return P3D_ERR_HIP;
   };
@@ -688,29 +714,28 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   if ((e = hipMalloc(&m->moving, (m->n_moving + 64) * sizeof(float))) != hipSuccess) return cleanup(e);
   if ((e = hipMemset(m->moving, 0, (m->n_moving + 64) * sizeof(float))) != hipSuccess) return cleanup(e);
-  if ((e = hipMalloc(&m->wt, m->n_wt * sizeof(float))) != hipSuccess) return cleanup(e);
-  if ((e = hipMemset(m->wt, 0, m->n_wt * sizeof(float))) != hipSuccess) return cleanup(e);
-  // workspace: per layer act, z, dz ([Bmax, N]); per layer stats; dout x2
-  const int64_t Bm = c.max_batch;
+  if ((e = hipMalloc(&m->wpk, m->n_wpk * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->wpk, 0, m->n_wpk * sizeof(float))) != hipSuccess) return cleanup(e);
+  // workspace: per hidden layer act, z, dz (packed [Bpad, L]); stats; dout x2
+  const int64_t Bp = m->Bpad;
   const int nl = (int)m->layers.size();
   int64_t need = 0;
-  for (int l = 0; l < nl - 1; ++l) need += 3 * pad64(Bm * L) + 2 * pad64(L);
-  need += 2 * pad64(Bm * L);
-  m->ws_elems = need;
+  for (int l = 0; l < nl - 1; ++l) need += 3 * pad64(Bp * L) + 2 * pad64(L);
+  need += 2 * pad64(Bp * L);
   if ((e = hipMalloc(&m->ws, need * sizeof(float))) != hipSuccess) return cleanup(e);
   if ((e = hipMemset(m->ws, 0, need * sizeof(float))) != hipSuccess) return cleanup(e);
   float* cur = m->ws;
   m->act.assign(nl, nullptr); m->z.assign(nl, nullptr); m->dz.assign(nl, nullptr);
   m->bmean.assign(nl, nullptr); m->bvar.assign(nl, nullptr);
   for (int l = 0; l < nl - 1; ++l) {
-    m->act[l] = cur; cur += pad64(Bm * L);
-    m->z[l] = cur; cur += pad64(Bm * L);
-    m->dz[l] = cur; cur += pad64(Bm * L);
+    m->act[l] = cur; cur += pad64(Bp * L);
+    m->z[l] = cur; cur += pad64(Bp * L);
+    m->dz[l] = cur; cur += pad64(Bp * L);
     m->bmean[l] = cur; cur += pad64(L);
     m->bvar[l] = cur; cur += pad64(L);
   }
-  m->dout[0] = cur; cur += pad64(Bm * L);
-  m->dout[1] = cur; cur += pad64(Bm * L);
+  m->dout[0] = cur; cur += pad64(Bp * L);
+  m->dout[1] = cur; cur += pad64(Bp * L);
   const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
@@ -731,12 +756,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
 
 extern "C" int p3d_destroy(p3d_model* m) {
   if (!m) return P3D_OK;
-  for (auto e : m->ev) (void)hipEventDestroy(e);
-  for (auto& p : m->flat) if (p) (void)hipFree(p);
-  if (m->moving) (void)hipFree(m->moving);
-  if (m->wt) (void)hipFree(m->wt);
-  if (m->ws) (void)hipFree(m->ws);
-  if (m->scratch) (void)hipFree(m->scratch);
+  free_all(m);
   delete m;
   return P3D_OK;
 }
@@ -787,12 +807,12 @@ extern "C" int p3d_flat_ptr(p3d_model* m, int32_t which, void** dptr, int64_t* n
 }
 
 static int refresh_derived(p3d_model* m, hipStream_t st) {
-  const int tiles = m->tt.tile_begin[m->tt.n];
+  const int64_t n4 = m->pt.begin[m->pt.n];
   {
-    ProfScope ps(m, "transpose", st);
-    k_transpose<<<tiles, 256, 0, st>>>(m->flat[0], m->wt, m->tt);
+    ProfScope ps(m, "pack", st);
+    k_pack<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(m->flat[0], m->wpk, m->pt);
   }
-  LAUNCH_CHECK("k_transpose");
+  LAUNCH_CHECK("k_pack");
   if (m->cfg.max_norm) {
     k_dot_partial<<<dim3(DOT_CHUNKS, m->wtab.n), 256, 0, st>>>(m->flat[0], m->flat[0], m->wtab, m->scratch);
     LAUNCH_CHECK("k_dot_partial");
@@ -808,14 +828,18 @@ extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
 }
 
 // ---- launch helpers ------------------------------------------------------------------
-template <int KIND>
+// Inference: 16x16 output tile per workgroup (grid 64 x 4 = 256 WGs for the 1024-wide
+// layers at B = 64), 16 waves split the contraction 16 ways (every operand load issued up
+// front).  BN-train: one workgroup owns all 64 rows of its 16 columns (batch statistics
+// are workgroup-local), 8 waves split the contraction.
+template <bool APK, bool YPK, int KIND>
 static void launch_fwd_k(const FwdArgs& a, bool whole_batch, hipStream_t st) {
   const int gx = (a.N + 15) / 16;
-  if (whole_batch) {  // BN-train: one workgroup owns all rows of its 16 columns
-    k_fwd<4, 4, 3, KIND><<<dim3(gx, 1), 256, 0, st>>>(a);
+  if (whole_batch) {
+    k_fwd<4, 8, 8, 2, APK, YPK, KIND><<<dim3(gx, 1), 512, 0, st>>>(a);
   } else {
     const int gy = (a.M + 15) / 16;
-    k_fwd<1, 4, 8, KIND><<<dim3(gx, gy), 256, 0, st>>>(a);
+    k_fwd<1, 16, 4, 2, APK, YPK, KIND><<<dim3(gx, gy), 1024, 0, st>>>(a);
   }
 }
 
@@ -823,38 +847,40 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind], st);
-  if (kind == 0) launch_fwd_k<0>(a, whole_batch, st);
-  else if (kind == 1) launch_fwd_k<1>(a, whole_batch, st);
-  else launch_fwd_k<2>(a, whole_batch, st);
+  if (kind == 0) launch_fwd_k<false, true, 0>(a, whole_batch, st);
+  else if (kind == 1) launch_fwd_k<true, true, 1>(a, whole_batch, st);
+  else launch_fwd_k<true, false, 2>(a, whole_batch, st);
   LAUNCH_CHECK("k_fwd");
   return P3D_OK;
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
-                           float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, void* stream) {
+extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
+                              float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row,
+                              void* stream) {
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_forward: null argument");
   const p3d_cfg& c = m->cfg;
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_forward: batch must be positive");
-  if (B > c.max_batch)
-    return fail(P3D_ERR_ARG, "p3d_forward: batch " + std::to_string(B) + " exceeds max_batch " +
-                                 std::to_string(c.max_batch));
+  if (ws_row < 0 || ws_row % 16 != 0) return fail(P3D_ERR_ARG, "p3d_forward_ex: ws_row must be a multiple of 16");
+  if (training && ws_row != 0) return fail(P3D_ERR_ARG, "p3d_forward_ex: training uses workspace rows from 0");
+  if (ws_row + B > c.max_batch)
+    return fail(P3D_ERR_ARG, "p3d_forward: batch " + std::to_string(B) + " (+ workspace row " + std::to_string(ws_row) +
+                                 ") exceeds max_batch " + std::to_string(c.max_batch));
   if (training && c.batch_norm && B > 64)
     return fail(P3D_ERR_ARG, "p3d_forward: training with batch_norm supports B <= 64 in this build");
   if (!(keep_prob > 0.f && keep_prob <= 1.f)) return fail(P3D_ERR_ARG, "keep_prob must be in (0, 1]");
   if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_forward: x must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
-  const int L = c.linear_size;
   const float decay = 1.0f - c.bn_momentum;
   const int nl = (int)m->layers.size();
+  const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
   const float* in = x;
-  int64_t ldin = c.input_size;
   for (int l = 0; l < nl; ++l) {
     const Layer& ly = m->layers[l];
     FwdArgs a{};
-    a.X = in; a.ldx = ldin;
-    a.Wt = m->wt + ly.wt; a.ldw = ly.K;
+    a.X = in; a.ldx = c.input_size;
+    a.Wf = m->wpk + ly.wf;
     a.bias = m->flat[0] + ly.b;
     a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
     a.M = (int)B; a.K = ly.K; a.N = ly.N;
@@ -872,13 +898,13 @@ extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, in
     a.seed = seed; a.ctr = ctr; a.site = ly.site; a.row_off = row_offset;
     // residual: second layer of block i adds the block input (layer l-2's output)
     const bool second = (l >= 1 && !last && ((l - 1) % 2 == 1));
-    if (c.residual && second) { a.res = (l - 2 >= 0) ? m->act[l - 2] : nullptr; a.ldr = L; }
+    if (c.residual && second) a.res = m->act[l - 2] + wsoff;
     if (last) { a.Y = y; a.ldy = ly.N; }
-    else { a.Y = m->act[l]; a.ldy = L; }
+    else { a.Y = m->act[l] + wsoff; a.ldy = 0; }
     const int kind = (l == 0) ? 0 : (last ? 2 : 1);
     const int rc = launch_fwd(m, a, kind, training && ly.bn, st);
     if (rc) return rc;
-    in = a.Y; ldin = a.ldy;
+    in = a.Y;
   }
   if (training) {
     m->have_cache = true;
@@ -890,6 +916,11 @@ extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, in
   return P3D_OK;
 }
 
+extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
+                           float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, void* stream) {
+  return p3d_forward_ex(m, x, B, y, training, keep_prob, seed, ctr, row_offset, 0, stream);
+}
+
 extern "C" int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, float* loss_dev, float* dy,
                        void* stream) {
   if (!y || !t) return fail(P3D_ERR_ARG, "p3d_mse: null argument");
@@ -899,11 +930,9 @@ extern "C" int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, flo
   return P3D_OK;
 }
 
-static int launch_wgrad(p3d_model* m, const float* X, int64_t ldx, const float* dZ, int64_t ldz, int M, int K,
-                        int N, float* dW, float* db, hipStream_t st) {
-  WgradArgs a{X, ldx, dZ, ldz, M, K, N, dW, db};
+static int launch_wgrad(p3d_model* m, const WgradArgs& a, hipStream_t st) {
   ProfScope ps(m, "wgrad", st);
-  k_wgrad<<<dim3((N + 63) / 64, (K + 63) / 64), 256, 0, st>>>(a);
+  k_wgrad<<<dim3((a.N + 63) / 64, (a.K + 63) / 64), 256, 0, st>>>(a);
   LAUNCH_CHECK("k_wgrad");
   return P3D_OK;
 }
@@ -914,41 +943,40 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (B != m->B_cached) return fail(P3D_ERR_ARG, "p3d_backward: batch differs from the training forward");
   if (B > 64) return fail(P3D_ERR_ARG, "p3d_backward: B <= 64 in this build");
   const p3d_cfg& c = m->cfg;
+  if (c.output_size % 16 != 0 || !aligned16(dy))
+    return fail(P3D_ERR_ARG, "p3d_backward: output_size must be a multiple of 16 and dy 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
-  const int L = c.linear_size;
   const int nl = (int)m->layers.size();
   float* grads = m->flat[1];
   const float* params = m->flat[0];
-  // layer l's input activation
-  auto input_of = [&](int l) -> const float* { return l == 0 ? m->x_cached : m->act[l - 1]; };
-  auto ld_in = [&](int l) -> int64_t { return l == 0 ? c.input_size : L; };
-  // Walk layers from the output back.  grad_in = gradient wrt layer l's z.
-  const float* dz_cur = dy;      // gradient wrt z of current layer l
-  int64_t ldz_cur = c.output_size;
+  const float* dz_cur = dy;   // gradient wrt z of the current layer l
+  bool dz_pk = false;         // dy is row-major; every later dz is packed
   int dsel = 0;
-  const float* dres_next = nullptr;  // block-output gradient to add when differentiating A-layer
+  const float* dres_next = nullptr;  // block-output gradient to add when differentiating an A-layer
   for (int l = nl - 1; l >= 0; --l) {
     const Layer& ly = m->layers[l];
-    // weight gradient of layer l
-    int rc = launch_wgrad(m, input_of(l), ld_in(l), dz_cur, ldz_cur, (int)B, ly.K, ly.N, grads + ly.w, grads + ly.b, st);
+    WgradArgs wa{};
+    wa.X = (l == 0) ? m->x_cached : m->act[l - 1]; wa.ldx = c.input_size; wa.xpk = (l != 0);
+    wa.dZ = dz_cur; wa.ldz = ly.N; wa.zpk = dz_pk;
+    wa.M = (int)B; wa.K = ly.K; wa.N = ly.N;
+    wa.dW = grads + ly.w; wa.db = grads + ly.b;
+    int rc = launch_wgrad(m, wa, st);
     if (rc) return rc;
     if (l == 0) break;
-    // data gradient into layer l-1
     const Layer& pv = m->layers[l - 1];
     BwdArgs a{};
-    a.dZ = dz_cur; a.ldz = ldz_cur;
-    a.W = params + ly.w; a.ldw = ly.N;
+    a.dZ = dz_cur; a.ldz = ly.N;
+    a.Wd = m->wpk + ly.wd; a.ngB = (ly.N + 15) / 16;
     a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
     a.M = (int)B; a.K = ly.K; a.N = ly.N;
     const bool is_out = (l == nl - 1);
     const bool is_A = !is_out && ((l - 1) % 2 == 0);   // first layer of a block
-    // the output of layer l-1 is a block output when l-1 is a B-layer (or the input layer)
     if (c.residual) {
-      if (is_out) {  // d(last block out): store raw for the block's residual
-        a.draw = m->dout[dsel]; a.ldraw = L;
-      } else if (is_A) {  // dX of a block input = dZ*W^T + d(block output)
-        a.dres = dres_next; a.ldres = L;
-        if (l - 1 >= 1) { a.draw = m->dout[dsel]; a.ldraw = L; }
+      if (is_out) {
+        a.draw = m->dout[dsel];              // d(last block output): kept for its residual
+      } else if (is_A) {
+        a.dres = dres_next;                  // dX of a block input = dZ*W^T + d(block output)
+        if (l - 1 >= 1) a.draw = m->dout[dsel];
       }
     }
     a.prev = 1;
@@ -958,19 +986,18 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     a.eps = c.bn_eps;
     a.relu = pv.relu;
     a.keep = m->keep; a.seed = m->seed; a.ctr = m->ctr; a.site = pv.site; a.row_off = m->row_off;
-    a.dz = m->dz[l - 1]; a.lddz = L;
+    a.dz = m->dz[l - 1];
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
-    if ((a.N % 16) != 0 || !aligned16(a.dZ) || (a.ldz % 4) != 0 || (a.ldw % 4) != 0)
-      return fail(P3D_ERR_ARG, "p3d_backward: output_size must be a multiple of 16 in this build");
     {
       ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden", st);
-      if (is_out) k_dgrad<4, 3, 2><<<dim3((a.K + 15) / 16, 1), 256, 0, st>>>(a);
-      else k_dgrad<4, 3, 1><<<dim3((a.K + 15) / 16, 1), 256, 0, st>>>(a);
+      const dim3 grid((a.K + 15) / 16, 1);
+      if (dz_pk) k_dgrad<8, 8, 2, true, 1><<<grid, 512, 0, st>>>(a);
+      else k_dgrad<8, 8, 2, false, 2><<<grid, 512, 0, st>>>(a);
     }
     LAUNCH_CHECK("k_dgrad");
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
     dz_cur = m->dz[l - 1];
-    ldz_cur = L;
+    dz_pk = true;
   }
   if (c.max_norm) {
     // G (dL/dW_eff) -> dL/dW through clip_by_norm
@@ -995,7 +1022,8 @@ extern "C" int p3d_adam_step(p3d_model* m, float lr, void* stream) {
   if (blocks > 2048) blocks = 2048;
   {
     ProfScope ps(m, "adam", st);
-  k_adam<<<blocks, 256, 0, st>>>(m->flat[0], m->flat[2], m->flat[3], m->flat[1], n4, alpha, 1.0f - b1, 1.0f - b2, eps);
+    k_adam<<<blocks, 256, 0, st>>>(m->flat[0], m->flat[2], m->flat[3], m->flat[1], n4, alpha, 1.0f - b1,
+                                   1.0f - b2, eps);
   }
   LAUNCH_CHECK("k_adam");
   m->b1p = m->b1p * b1;

@@ -359,16 +359,19 @@ class LinearModel(object):
             t = t.to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
         return t
 
-    def forward_device(self, x, training=False, keep_prob=1.0, out=None, ctr=None):
-        """Device-resident forward: returns outputs [B, output_size] (no host sync)."""
+    def forward_device(self, x, training=False, keep_prob=1.0, out=None, ctr=None, ws_row=0):
+        """Device-resident forward: returns outputs [B, output_size] (no host sync).
+
+        ``ws_row`` (inference only) selects the workspace rows this call uses, so that
+        independent batches on different streams can run concurrently."""
         x = self._as_dev(x, self.input_size, "enc_in")
         B = x.shape[0]
         if out is None:
             out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
         if ctr is None:
             ctr = self.get_step()[0]
-        check(lib().p3d_forward(self._h, ptr(x), B, ptr(out), int(bool(training)), float(keep_prob),
-                                self.seed, int(ctr), self.rank * B, self.stream()), "p3d_forward")
+        check(lib().p3d_forward_ex(self._h, ptr(x), B, ptr(out), int(bool(training)), float(keep_prob),
+                                   self.seed, int(ctr), self.rank * B, int(ws_row), self.stream()), "p3d_forward")
         return out
 
     def loss_device(self, y, t, dy=None):

@@ -93,6 +93,13 @@ int p3d_params_updated(p3d_model* m, void* stream);
 int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
                 float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, void* stream);
 
+/* p3d_forward on workspace rows [ws_row, ws_row + B) (ws_row a multiple of 16,
+ * inference only): independent batches issued on different streams with disjoint
+ * workspace rows run concurrently; results are bit-identical to p3d_forward. */
+int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
+                   float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row,
+                   void* stream);
+
 /* MSE loss of linear_model.py:129 and its gradient: loss = mean((y-t)^2) over
  * B*D, dy = (1/(B*D)) * 2*(y-t).  loss_dev: one device float (may be NULL),
  * dy may be NULL. */
