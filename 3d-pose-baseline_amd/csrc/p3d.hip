@@ -921,6 +921,33 @@ extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, in
   return p3d_forward_ex(m, x, B, y, training, keep_prob, seed, ctr, row_offset, 0, stream);
 }
 
+// Timing hook: `reps` back-to-back launches of hidden layer `layer` (1 .. 2N) of the
+// inference forward on workspace rows [0, B) (act[layer-1] -> act[layer]).  Idempotent.
+extern "C" int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  const p3d_cfg& c = m->cfg;
+  const int nl = (int)m->layers.size();
+  if (layer < 1 || layer > nl - 2) return fail(P3D_ERR_ARG, "p3d_time_layer: layer must be a hidden layer");
+  if (B <= 0 || B > c.max_batch) return fail(P3D_ERR_ARG, "p3d_time_layer: bad batch");
+  const Layer& ly = m->layers[layer];
+  FwdArgs a{};
+  a.X = m->act[layer - 1]; a.Wf = m->wpk + ly.wf; a.bias = m->flat[0] + ly.b;
+  a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
+  a.M = (int)B; a.K = ly.K; a.N = ly.N;
+  if (ly.bn) {
+    a.bn = 1; a.gamma = m->flat[0] + ly.gamma; a.beta = m->flat[0] + ly.beta;
+    a.mmean = m->moving + ly.mmean; a.mvar = m->moving + ly.mvar; a.eps = c.bn_eps;
+  }
+  a.relu = 1; a.keep = 1.0f; a.site = ly.site;
+  if (c.residual && ((layer - 1) % 2 == 1)) a.res = m->act[layer - 2];
+  a.Y = m->act[layer];
+  for (int r = 0; r < reps; ++r) {
+    const int rc = launch_fwd(m, a, 1, false, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return P3D_OK;
+}
+
 extern "C" int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, float* loss_dev, float* dy,
                        void* stream) {
   if (!y || !t) return fail(P3D_ERR_ARG, "p3d_mse: null argument");

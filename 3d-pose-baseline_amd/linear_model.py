@@ -23,6 +23,7 @@ import time
 import numpy as np
 
 import _p3d
+import dist_utils
 from _p3d import check, lib, ptr
 
 HUMAN_2D_SIZE = 16 * 2
@@ -340,10 +341,8 @@ class LinearModel(object):
                                      float(st["beta2_power"])), "p3d_set_step")
 
     def broadcast_parameters(self):
-        import torch.distributed as dist
-        for key in ("params", "moving", "adam_m", "adam_v"):
-            if self.flat[key] is not None:
-                dist.broadcast(self.flat[key], src=0)
+        """Rank 0's variables to every rank (start of data-parallel training)."""
+        dist_utils.broadcast_([self.flat[k] for k in ("params", "moving", "adam_m", "adam_v")], src=0)
         self.params_updated()
 
     # ------------------------------------------------------------------ device-side API
@@ -417,13 +416,7 @@ class LinearModel(object):
         return loss, y
 
     def _allreduce_grads(self):
-        import torch.distributed as dist
-        g = self.flat["grads"]
-        if dist.get_backend() == "nccl":
-            dist.all_reduce(g, op=dist.ReduceOp.AVG)
-        else:
-            dist.all_reduce(g, op=dist.ReduceOp.SUM)
-            g.div_(self.world)
+        dist_utils.allreduce_mean_(self.flat["grads"])
 
     # ------------------------------------------------------------------ reference API
     def step(self, session, encoder_inputs, decoder_outputs, dropout_keep_prob, isTraining=True):
@@ -450,34 +443,9 @@ class LinearModel(object):
             return lv, Summary("loss/loss", lv), out
 
     def get_all_batches(self, data_x, data_y, camera_frame, training=True):
-        """src/linear_model.py:247-300: concatenate in dict order, permute when training,
-        drop the ``n % batch_size`` tail, split into batches (float64 host arrays)."""
-        n = 0
-        for key2d in data_x.keys():
-            n += data_x[key2d].shape[0]
-        encoder_inputs = np.zeros((n, self.input_size), dtype=float)
-        decoder_outputs = np.zeros((n, self.output_size), dtype=float)
-        idx = 0
-        for key2d in data_x.keys():
-            (subj, b, fname) = key2d
-            key3d = key2d if camera_frame else (subj, b, '{0}.h5'.format(fname.split('.')[0]))
-            key3d = (subj, b, fname[:-3]) if fname.endswith('-sh') and camera_frame else key3d
-            n2d = data_x[key2d].shape[0]
-            encoder_inputs[idx:idx + n2d, :] = data_x[key2d]
-            decoder_outputs[idx:idx + n2d, :] = data_y[key3d]
-            idx += n2d
-        if training:
-            perm = np.random.permutation(n)
-            encoder_inputs = encoder_inputs[perm, :]
-            decoder_outputs = decoder_outputs[perm, :]
-        n_extra = n % self.batch_size
-        if n_extra > 0:
-            encoder_inputs = encoder_inputs[:-n_extra, :]
-            decoder_outputs = decoder_outputs[:-n_extra, :]
-        n_batches = n // self.batch_size
-        if n_batches == 0:
-            return [], []
-        return np.split(encoder_inputs, n_batches), np.split(decoder_outputs, n_batches)
+        """src/linear_model.py:247-300 (see ``get_all_batches`` below)."""
+        return get_all_batches(data_x, data_y, camera_frame, self.batch_size, self.input_size,
+                               self.output_size, training)
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -490,3 +458,32 @@ class LinearModel(object):
             self.close()
         except Exception:
             pass
+
+
+def get_all_batches(data_x, data_y, camera_frame, batch_size, input_size=HUMAN_2D_SIZE, output_size=48,
+                    training=True):
+    """src/linear_model.py:247-300: concatenate the dict values in key order into float64
+    arrays, permute when training (np.random, unseeded like the reference), drop the
+    ``n % batch_size`` tail, split into batches."""
+    n = sum(v.shape[0] for v in data_x.values())
+    encoder_inputs = np.zeros((n, input_size), dtype=float)
+    decoder_outputs = np.zeros((n, output_size), dtype=float)
+    idx = 0
+    for key2d in data_x.keys():
+        (subj, b, fname) = key2d
+        key3d = key2d if camera_frame else (subj, b, '{0}.h5'.format(fname.split('.')[0]))
+        key3d = (subj, b, fname[:-3]) if fname.endswith('-sh') and camera_frame else key3d
+        n2d = data_x[key2d].shape[0]
+        encoder_inputs[idx:idx + n2d, :] = data_x[key2d]
+        decoder_outputs[idx:idx + n2d, :] = data_y[key3d]
+        idx += n2d
+    if training:
+        perm = np.random.permutation(n)
+        encoder_inputs, decoder_outputs = encoder_inputs[perm, :], decoder_outputs[perm, :]
+    n_extra = n % batch_size
+    if n_extra > 0:
+        encoder_inputs, decoder_outputs = encoder_inputs[:-n_extra, :], decoder_outputs[:-n_extra, :]
+    n_batches = n // batch_size
+    if n_batches == 0:
+        return [], []
+    return np.split(encoder_inputs, n_batches), np.split(decoder_outputs, n_batches)

@@ -26,6 +26,7 @@ import numpy as np
 
 import _p3d
 import data_utils
+import dist_utils
 import linear_model
 from _p3d import check, lib, ptr
 
@@ -219,19 +220,15 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
     ({action: mm}, average_mm) with the reference's unweighted Average.
     """
     import torch
-    import torch.distributed as dist
     flags = flags or FLAGS
-    dist_on = dist.is_available() and dist.is_initialized()
-    rank = dist.get_rank() if dist_on else 0
-    world = dist.get_world_size() if dist_on else 1
+    _, rank, world = dist_utils.dist_state()
     table = torch.zeros((len(actions), 19), dtype=torch.float64, device=model.device)
     with torch.cuda.device(model.device):
         for ai, action in enumerate(actions):
             enc, dec = model.get_all_batches(get_action_subset(test_set_2d, action),
                                              get_action_subset(test_set_3d, action), camera_frame,
                                              training=False)
-            nb = len(enc)
-            lo, hi = (nb * rank) // world, (nb * (rank + 1)) // world
+            lo, hi = dist_utils.shard_range(len(enc), rank, world)
             acc = MPJPE(model, data_mean_3d, data_std_3d, dim_to_use_3d, flags.predict_14, flags.procrustes)
             if hi > lo:
                 X = torch.from_numpy(_stack(enc[lo:hi], model.input_size)).to(model.device)
@@ -240,8 +237,7 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
             table[ai, :17] = acc.joint_sum
             table[ai, 17] = float(acc.frames)
             table[ai, 18] = acc.loss_sum[0]
-        if dist_on and world > 1:
-            dist.all_reduce(table, op=dist.ReduceOp.SUM)
+        dist_utils.allreduce_sum_(table)
         t = table.cpu().numpy()
     errs = {}
     for ai, action in enumerate(actions):

@@ -137,6 +137,10 @@ int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96
 int p3d_profile_start(p3d_model* m, int32_t max_launches);
 int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len);
 
+/* Roofline timing hook: `reps` back-to-back launches of hidden layer `layer`
+ * (1 .. 2*num_layers) of the inference forward over workspace rows [0, B). */
+int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
