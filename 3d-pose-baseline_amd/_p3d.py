@@ -14,6 +14,7 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uin
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libp3d.so")
 
+P3D_CTR_GLOBAL_STEP = 0xFFFFFFFFFFFFFFFF
 P3D_DTYPE_F32 = 0
 P3D_DTYPE_BF16 = 1
 
@@ -47,6 +48,7 @@ SIGNATURES = [
     ("p3d_mse", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_backward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_adam_step", c_int32, [c_void_p, c_float, c_void_p]),
+    ("p3d_adam_step_decay", c_int32, [c_void_p, c_float, c_float, c_float, c_void_p]),
     ("p3d_get_step", c_int32, [c_void_p, POINTER(c_int64), POINTER(c_float), POINTER(c_float)]),
     ("p3d_set_step", c_int32, [c_void_p, c_int64, c_float, c_float]),
     ("p3d_mpjpe_accum", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,

@@ -40,6 +40,7 @@ struct FwdArgs {
   float* mean_save; float* var_save;
   int relu;
   float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
+  const int64_t* ctr_dev;         // if set, dropout counter = *ctr_dev (device global_step)
   const float* res;               // residual added after dropout, packed [M, N]
   float* Y; int64_t ldy;          // packed (hidden) or row-major (output layer)
 };
@@ -58,7 +59,9 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   const int ngN = (p.N + 15) >> 4;
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
+  uint64_t ctr = p.ctr;
   if (w == 0) {
+    if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     b = p.bias[cc];
     if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
 #pragma unroll
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       float y = p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
       if (p.keep < 1.0f) {
-        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + row, col);
+        const float u = p3d_uniform(p.seed, ctr, p.site, p.row_off + row, col);
         y = (y / p.keep) * p3d_dropout_mask(p.keep, u);
       }
       if (p.res) y += rv[s][r];
@@ -151,6 +154,7 @@ struct BwdArgs {
   int bn; const float* z; const float* mean; const float* var;   // prev layer: z packed [M,K]
   const float* gamma; const float* beta; float eps;
   int relu; float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
+  const int64_t* ctr_dev;
   float* dz;                      // packed [M, K]: gradient wrt prev layer's z
   float* dgamma; float* dbeta;    // [K]
 };
@@ -168,7 +172,9 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   const int ngK = p.K >> 4;
   // prefetch the epilogue's per-column and per-element operands
   float mean = 0.f, var = 1.f, gam = 1.f, bet = 0.f, zz[RS][4], dr[RS][4];
+  uint64_t ctr = p.ctr;
   if (w == 0) {
+    if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     if (p.prev && p.bn) { mean = p.mean[cc]; var = p.var[cc]; gam = p.gamma[cc]; bet = p.beta[cc]; }
 #pragma unroll
     for (int s = 0; s < RS; ++s)
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
       const bool ok = row < p.M;
       float gg = g[s][r];
       if (p.keep < 1.0f) {
-        const float u = p3d_uniform(p.seed, p.ctr, p.site, p.row_off + row, cc);
+        const float u = p3d_uniform(p.seed, ctr, p.site, p.row_off + row, cc);
         gg = (gg * p3d_dropout_mask(p.keep, u)) / p.keep;
       }
       const float a = p.bn ? zz[s][r] * inv + shift : zz[s][r];
@@ -327,35 +333,168 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
 }
 
 // =====================================================================================
-// TF1 ApplyAdam over the flat trainable buffer (float4 vectorised)
+// TF1 ApplyAdam fused with the weight re-pack (one launch per optimizer step)
+//   alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+//   w -= (m*alpha)/(sqrt(v)+eps)                          (linear_model.py:137,145)
+// Step state (global_step, beta powers) lives on the device so that whole training
+// steps can be graph-captured: every block reads it first; the last block to finish
+// (arrival counter) advances it.  lr is either given (lr_host >= 0) or the TF
+// exponential decay lr0 * rate^(global_step / steps) computed on the device.
+// Weight matrices are processed in 16x16 tiles (64 threads each) so that the updated
+// tile is also written in both fragment-major layouts (Wd directly, Wf via an LDS
+// transpose); 1-D tensors (biases, gamma, beta) are updated float-wise.
 // =====================================================================================
-__global__ __launch_bounds__(256) void k_adam(float* __restrict__ w, float* __restrict__ m,
-                                              float* __restrict__ v, const float* __restrict__ g,
-                                              int64_t n4, float alpha, float one_m_b1, float one_m_b2,
-                                              float eps) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t e = idx; e < n4; e += stride) {
-    f32x4 gg = ((const f32x4*)g)[e];
-    f32x4 mm = ((f32x4*)m)[e];
-    f32x4 vv = ((f32x4*)v)[e];
-    f32x4 ww = ((f32x4*)w)[e];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      mm[c] += (gg[c] - mm[c]) * one_m_b1;
-      vv[c] += (gg[c] * gg[c] - vv[c]) * one_m_b2;
-      ww[c] -= (mm[c] * alpha) / (sqrtf(vv[c]) + eps);
-    }
-    ((f32x4*)m)[e] = mm;
-    ((f32x4*)v)[e] = vv;
-    ((f32x4*)w)[e] = ww;
+#define P3D_MAX_W 40
+#define P3D_MAX_V 64
+struct StepState {
+  int64_t global_step;
+  float beta1_power, beta2_power;
+  unsigned int arrivals;
+  unsigned int pad[3];
+};
+
+struct AdamTable {
+  int nw, nv;
+  int K[P3D_MAX_W], N[P3D_MAX_W];
+  int64_t off[P3D_MAX_W], wf[P3D_MAX_W], wd[P3D_MAX_W];
+  int tile_begin[P3D_MAX_W + 1];   // 64x64 tiles, prefix over weights
+  int64_t voff[P3D_MAX_V];
+  int vlen[P3D_MAX_V];
+  int vbegin[P3D_MAX_V + 1];       // 1024-element chunks, prefix over vectors
+};
+
+struct AdamArgs {
+  float* w; float* m; float* v; const float* g;
+  float* wpk;
+  StepState* st;
+  float lr_host;        // >= 0: use as lr; < 0: device exponential decay of lr0
+  float lr0, decay_steps, decay_rate;
+  float b1, b2, eps;
+  int wblocks;          // blocks spent on weight tiles (one 64x64 tile each)
+};
+
+__device__ __forceinline__ void p3d_adam1(float& w, float& m, float& v, float g, float alpha, float omb1,
+                                          float omb2, float eps) {
+  m += (g - m) * omb1;
+  v += (g * g - v) * omb2;
+  w -= (m * alpha) / (sqrtf(v) + eps);
+}
+
+// One 64x64 weight tile per 256-thread block: 16 threads x float4 per 256-B row segment;
+// the updated tile is staged in LDS and written as 16 Wd and 16 Wf fragment-major 1 KB
+// chunks (64 lanes x float4 each, fully contiguous).
+__global__ __launch_bounds__(256) void k_adam_pack(AdamArgs a, AdamTable tb) {
+  __shared__ float tile[64][65];
+  __shared__ float s_alpha;
+  if (threadIdx.x == 0) {
+    const float b1p = a.st->beta1_power, b2p = a.st->beta2_power;
+    float lr = a.lr_host;
+    if (lr < 0.f) lr = a.lr0 * powf(a.decay_rate, (float)a.st->global_step / a.decay_steps);
+    s_alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   }
+  __syncthreads();
+  const float alpha = s_alpha, omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < a.wblocks) {
+    const int tile_id = blockIdx.x;
+    int wi = 0;
+    while (wi + 1 < tb.nw && tile_id >= tb.tile_begin[wi + 1]) ++wi;
+    const int K = tb.K[wi], N = tb.N[wi];
+    const int tnc = (N + 63) >> 6;
+    const int local = tile_id - tb.tile_begin[wi];
+    const int k0 = (local / tnc) * 64, n0 = (local % tnc) * 64;
+    const bool vec = (N & 3) == 0;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+      const int k = k0 + r, n = n0 + c;
+      float wn[4] = {0.f, 0.f, 0.f, 0.f};
+      if (k < K) {
+        const int64_t base = tb.off[wi] + (int64_t)k * N + n;
+        if (vec && n + 3 < N) {
+          f32x4 ww = *(f32x4*)(a.w + base), mm = *(f32x4*)(a.m + base), vv = *(f32x4*)(a.v + base);
+          const f32x4 gg = *(const f32x4*)(a.g + base);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float w1 = ww[e], m1 = mm[e], v1 = vv[e];
+            p3d_adam1(w1, m1, v1, gg[e], alpha, omb1, omb2, a.eps);
+            ww[e] = w1; mm[e] = m1; vv[e] = v1; wn[e] = w1;
+          }
+          *(f32x4*)(a.w + base) = ww; *(f32x4*)(a.m + base) = mm; *(f32x4*)(a.v + base) = vv;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) {
+              float ww = a.w[base + e], mm = a.m[base + e], vv = a.v[base + e];
+              p3d_adam1(ww, mm, vv, a.g[base + e], alpha, omb1, omb2, a.eps);
+              a.w[base + e] = ww; a.m[base + e] = mm; a.v[base + e] = vv;
+              wn[e] = ww;
+            }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];
+    }
+    __syncthreads();
+    // 16 sub-tiles of 16x16; thread = (sub-tile group of 4 threads? no: lane of a chunk)
+    const int NP = (N + 15) & ~15;
+    const int ngf = K >> 4, ngd = NP >> 4;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int sub = it * 4 + (tid >> 6), l = tid & 63;
+      const int sk = sub >> 2, sn = sub & 3;             // 16x16 sub-tile within the 64x64 tile
+      const int kt = (k0 >> 4) + sk, nt = (n0 >> 4) + sn;
+      if (16 * kt >= K || 16 * nt >= NP) continue;
+      const int i = l & 15, q = l >> 4;
+      // Wd (rows k, cols n): element (16kt+i, 16nt+4q+e)
+      const f32x4 od = f32x4{tile[16 * sk + i][16 * sn + 4 * q], tile[16 * sk + i][16 * sn + 4 * q + 1],
+                             tile[16 * sk + i][16 * sn + 4 * q + 2], tile[16 * sk + i][16 * sn + 4 * q + 3]};
+      *(f32x4*)(a.wpk + tb.wd[wi] + ((int64_t)(kt * ngd + nt) * 64 + l) * 4) = od;
+      // Wf (rows n, cols k): element (16nt+i, 16kt+4q+e)
+      const f32x4 of = f32x4{tile[16 * sk + 4 * q][16 * sn + i], tile[16 * sk + 4 * q + 1][16 * sn + i],
+                             tile[16 * sk + 4 * q + 2][16 * sn + i], tile[16 * sk + 4 * q + 3][16 * sn + i]};
+      *(f32x4*)(a.wpk + tb.wf[wi] + ((int64_t)(nt * ngf + kt) * 64 + l) * 4) = of;
+    }
+  } else {
+    const int chunk = blockIdx.x - a.wblocks;
+    if (chunk < tb.vbegin[tb.nv]) {
+      int vi = 0;
+      while (vi + 1 < tb.nv && chunk >= tb.vbegin[vi + 1]) ++vi;
+      const int e0 = (chunk - tb.vbegin[vi]) * 1024 + 4 * tid;
+      const int64_t i = tb.voff[vi] + e0;
+      if (e0 + 3 < tb.vlen[vi]) {   // vectors start 256-B aligned in the flat buffer
+        f32x4 ww = *(f32x4*)(a.w + i), mm = *(f32x4*)(a.m + i), vv = *(f32x4*)(a.v + i);
+        const f32x4 gg = *(const f32x4*)(a.g + i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float w1 = ww[e], m1 = mm[e], v1 = vv[e];
+          p3d_adam1(w1, m1, v1, gg[e], alpha, omb1, omb2, a.eps);
+          ww[e] = w1; mm[e] = m1; vv[e] = v1;
+        }
+        *(f32x4*)(a.w + i) = ww; *(f32x4*)(a.m + i) = mm; *(f32x4*)(a.v + i) = vv;
+      } else {
+        for (int e = 0; e < 4 && e0 + e < tb.vlen[vi]; ++e) {
+          float ww = a.w[i + e], mm = a.m[i + e], vv = a.v[i + e];
+          p3d_adam1(ww, mm, vv, a.g[i + e], alpha, omb1, omb2, a.eps);
+          a.w[i + e] = ww; a.m[i + e] = mm; a.v[i + e] = vv;
+        }
+      }
+    }
+  }
+}
+
+// Advance the device step state after the optimizer (one thread; stream-ordered after
+// every block of k_adam_pack has read the old state).
+__global__ void k_step_advance(StepState* st, float b1, float b2) {
+  st->beta1_power = st->beta1_power * b1;
+  st->beta2_power = st->beta2_power * b2;
+  st->global_step = st->global_step + 1;
 }
 
 // =====================================================================================
 // pack every weight W [K, N] into Wf (rows n, cols k) and Wd (rows k, cols n padded)
+// (after the host writes parameters; the optimizer re-packs inside k_adam_pack)
 // =====================================================================================
-#define P3D_MAX_W 40
 struct PackTable {
   int n;
   int K[P3D_MAX_W], N[P3D_MAX_W];
@@ -561,6 +700,9 @@ struct p3d_model {
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
+  AdamTable at;
+  int adam_blocks = 0;
+  StepState* dstate = nullptr;  // device: global_step, beta powers, arrival counter
   DotTable wtab;
   // per-layer workspace (packed, Bpad rows)
   std::vector<float*> act;    // output of layer l (layer B_i holds the block output)
@@ -575,8 +717,7 @@ struct p3d_model {
   float keep = 1.f;
   uint64_t seed = 0, ctr = 0;
   int64_t row_off = 0;
-  int64_t global_step = 0;
-  float b1p = 0.9f, b2p = 0.999f;
+  const int64_t* ctr_dev = nullptr;   // cached training-forward counter source
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -606,6 +747,7 @@ void free_all(p3d_model* m) {
   if (m->wpk) (void)hipFree(m->wpk);
   if (m->ws) (void)hipFree(m->ws);
   if (m->scratch) (void)hipFree(m->scratch);
+  if (m->dstate) (void)hipFree(m->dstate);
 }
 }  // namespace
 
@@ -700,6 +842,32 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     m->wtab.n = t + 1;
   }
   m->pt.begin[m->pt.n] = f4;
+  // optimizer table: weight matrices as 16x16 tiles, everything else as 1-D vectors
+  {
+    AdamTable& at = m->at;
+    at.nw = 0; at.nv = 0;
+    int tiles = 0, vch = 0;
+    for (size_t l = 0; l < m->layers.size(); ++l) {
+      const Layer& ly = m->layers[l];
+      const int t = at.nw++;
+      at.K[t] = ly.K; at.N[t] = ly.N; at.off[t] = ly.w; at.wf[t] = ly.wf; at.wd[t] = ly.wd;
+      at.tile_begin[t] = tiles;
+      tiles += ((ly.K + 63) / 64) * ((ly.N + 63) / 64);
+    }
+    at.tile_begin[at.nw] = tiles;
+    for (const Tensor& tn : m->tensors) {
+      if (tn.kind != 0) continue;
+      bool is_w = false;
+      for (const Layer& ly : m->layers) if (ly.w == tn.off) is_w = true;
+      if (is_w) continue;
+      if (at.nv >= P3D_MAX_V) { delete m; return fail(P3D_ERR_ARG, "too many parameter vectors"); }
+      at.voff[at.nv] = tn.off; at.vlen[at.nv] = (int)tn.numel; at.vbegin[at.nv] = vch;
+      vch += (int)((tn.numel + 1023) / 1024);
+      at.nv++;
+    }
+    at.vbegin[at.nv] = vch;
+    m->adam_blocks = tiles + vch;
+  }
 
   auto cleanup = [&](hipError_t e) {
     g_err = std::string("p3d_create: ") + hipGetErrorString(e);
@@ -738,6 +906,12 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   m->dout[1] = cur; cur += pad64(Bp * L);
   const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
+  {
+    StepState s0{};
+    s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
+    if ((e = hipMalloc(&m->dstate, sizeof(StepState))) != hipSuccess) return cleanup(e);
+    if ((e = hipMemcpy(m->dstate, &s0, sizeof(StepState), hipMemcpyHostToDevice)) != hipSuccess) return cleanup(e);
+  }
   m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
   m->gw = m->wsq + 64;
   // TF defaults: BN gamma = 1, moving_variance = 1 (beta/mean = 0 already)
@@ -896,6 +1070,7 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
     a.relu = ly.relu;
     a.keep = last ? 1.0f : keep_prob;
     a.seed = seed; a.ctr = ctr; a.site = ly.site; a.row_off = row_offset;
+    a.ctr_dev = (ctr == P3D_CTR_GLOBAL_STEP) ? &m->dstate->global_step : nullptr;
     // residual: second layer of block i adds the block input (layer l-2's output)
     const bool second = (l >= 1 && !last && ((l - 1) % 2 == 1));
     if (c.residual && second) a.res = m->act[l - 2] + wsoff;
@@ -912,6 +1087,7 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
     m->B_cached = B;
     m->keep = keep_prob;
     m->seed = seed; m->ctr = ctr; m->row_off = row_offset;
+    m->ctr_dev = (ctr == P3D_CTR_GLOBAL_STEP) ? &m->dstate->global_step : nullptr;
   }
   return P3D_OK;
 }
@@ -1013,6 +1189,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     a.eps = c.bn_eps;
     a.relu = pv.relu;
     a.keep = m->keep; a.seed = m->seed; a.ctr = m->ctr; a.site = pv.site; a.row_off = m->row_off;
+    a.ctr_dev = m->ctr_dev;
     a.dz = m->dz[l - 1];
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
     {
@@ -1038,40 +1215,58 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   return P3D_OK;
 }
 
+static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st) {
+  AdamArgs a{};
+  a.w = m->flat[0]; a.g = m->flat[1]; a.m = m->flat[2]; a.v = m->flat[3];
+  a.wpk = m->wpk; a.st = m->dstate;
+  a.lr_host = lr_host; a.lr0 = lr0; a.decay_steps = steps; a.decay_rate = rate;
+  a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
+  a.wblocks = m->at.tile_begin[m->at.nw];
+  {
+    ProfScope ps(m, "adam_pack", st);
+    k_adam_pack<<<m->adam_blocks, 256, 0, st>>>(a, m->at);
+  }
+  LAUNCH_CHECK("k_adam_pack");
+  k_step_advance<<<1, 1, 0, st>>>(m->dstate, a.b1, a.b2);
+  LAUNCH_CHECK("k_step_advance");
+  if (m->cfg.max_norm) {
+    k_dot_partial<<<dim3(DOT_CHUNKS, m->wtab.n), 256, 0, st>>>(m->flat[0], m->flat[0], m->wtab, m->scratch);
+    LAUNCH_CHECK("k_dot_partial");
+    k_dot_final<<<1, 64, 0, st>>>(m->scratch, m->wtab.n, m->wsq);
+    LAUNCH_CHECK("k_dot_final");
+  }
+  return P3D_OK;
+}
+
 extern "C" int p3d_adam_step(p3d_model* m, float lr, void* stream) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
-  hipStream_t st = (hipStream_t)stream;
-  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
-  // alpha in fp32 exactly as TF's ApplyAdam functor computes it
-  const float alpha = lr * sqrtf(1.0f - m->b2p) / (1.0f - m->b1p);
-  const int64_t n4 = m->n_flat / 4;
-  int blocks = (int)((n4 + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
-  {
-    ProfScope ps(m, "adam", st);
-    k_adam<<<blocks, 256, 0, st>>>(m->flat[0], m->flat[2], m->flat[3], m->flat[1], n4, alpha, 1.0f - b1,
-                                   1.0f - b2, eps);
-  }
-  LAUNCH_CHECK("k_adam");
-  m->b1p = m->b1p * b1;
-  m->b2p = m->b2p * b2;
-  m->global_step += 1;
-  return refresh_derived(m, st);
+  if (!(lr >= 0.f)) return fail(P3D_ERR_ARG, "p3d_adam_step: lr must be >= 0");
+  return adam_launch(m, lr, 0.f, 1.f, 1.f, (hipStream_t)stream);
+}
+
+extern "C" int p3d_adam_step_decay(p3d_model* m, float lr0, float decay_steps, float decay_rate, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  if (!(decay_steps > 0.f)) return fail(P3D_ERR_ARG, "p3d_adam_step_decay: decay_steps must be > 0");
+  return adam_launch(m, -1.f, lr0, decay_steps, decay_rate, (hipStream_t)stream);
 }
 
 extern "C" int p3d_get_step(const p3d_model* m, int64_t* gs, float* b1p, float* b2p) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
-  if (gs) *gs = m->global_step;
-  if (b1p) *b1p = m->b1p;
-  if (b2p) *b2p = m->b2p;
+  StepState s{};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&s, m->dstate, sizeof(StepState), hipMemcpyDeviceToHost));
+  if (gs) *gs = s.global_step;
+  if (b1p) *b1p = s.beta1_power;
+  if (b2p) *b2p = s.beta2_power;
   return P3D_OK;
 }
 
 extern "C" int p3d_set_step(p3d_model* m, int64_t gs, float b1p, float b2p) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
-  m->global_step = gs;
-  m->b1p = b1p;
-  m->b2p = b2p;
+  StepState s{};
+  s.global_step = gs; s.beta1_power = b1p; s.beta2_power = b2p; s.arrivals = 0;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(m->dstate, &s, sizeof(StepState), hipMemcpyHostToDevice));
   return P3D_OK;
 }
 

@@ -368,7 +368,7 @@ class LinearModel(object):
         if out is None:
             out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
         if ctr is None:
-            ctr = self.get_step()[0]
+            ctr = _p3d.P3D_CTR_GLOBAL_STEP if training else 0
         check(lib().p3d_forward_ex(self._h, ptr(x), B, ptr(out), int(bool(training)), float(keep_prob),
                                    self.seed, int(ctr), self.rank * B, int(ws_row), self.stream()), "p3d_forward")
         return out
@@ -390,15 +390,16 @@ class LinearModel(object):
         B = x.shape[0]
         if B > self.max_batch:
             raise ValueError("batch %d exceeds max_batch %d" % (B, self.max_batch))
-        gs = self.get_step()[0]
         self._x_keep = x  # the library differentiates this buffer in p3d_backward
-        y = self.forward_device(x, True, keep_prob, out=out, ctr=gs)
+        # dropout counter, lr decay and the Adam beta powers all come from the device-side
+        # step state, so this sequence is capturable in a HIP graph
+        y = self.forward_device(x, True, keep_prob, out=out, ctr=_p3d.P3D_CTR_GLOBAL_STEP)
         dy = self._dy[:B]
         loss = self.loss_device(y, t, dy)
         check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
         if self.data_parallel:
             self._allreduce_grads()
-        check(lib().p3d_adam_step(self._h, exponential_decay(self.lr0, gs), self.stream()), "p3d_adam_step")
+        check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
         return loss, y
 
     def compute_gradients(self, x, t, keep_prob, ctr=None):

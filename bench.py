@@ -223,11 +223,19 @@ def bench_infer(args, rank, world):
     return value, dt, roof
 
 
-def bench_train(args, rank, world):
+def bench_train(args, rank, world, steps=None, warmup=None):
+    """cfg3: K training steps (fwd + MSE + bwd + [all-reduce] + fused TF1 Adam/re-pack) of
+    64 poses per GPU.  Single GPU: G steps captured in one HIP graph (all step state is
+    device-resident: dropout counter, lr decay, beta powers).  Data parallel: eager steps
+    with one RCCL all-reduce(AVG) of the 17.17 MB flat gradient per step."""
     import torch
+    steps = steps or args.steps
+    warmup = warmup if warmup is not None else args.warmup
     model, _ = make_model(data_parallel=world > 1)
     rng = np.random.default_rng(200 + rank)
     G = 16
+    while steps % G:
+        G -= 1
     X = torch.from_numpy(rng.standard_normal((G, BATCH, IN)).astype(np.float32)).cuda()
     T = torch.from_numpy(rng.standard_normal((G, BATCH, OUT)).astype(np.float32)).cuda()
     Y = torch.empty((BATCH, OUT), dtype=torch.float32, device="cuda")
@@ -236,25 +244,44 @@ def bench_train(args, rank, world):
         for i in range(k):
             model.train_step_device(X[i % G], T[i % G], 0.5, out=Y)
 
-    run(args.warmup)
+    use_graph = world == 1 or args.train_graph
+    run(max(2, warmup // 4))
+    torch.cuda.synchronize()
+    if use_graph:
+        s0 = torch.cuda.Stream()
+        s0.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s0):
+            run(G)
+        torch.cuda.current_stream().wait_stream(s0)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            run(G)
+        fn, per = graph.replay, G
+    else:
+        fn, per = (lambda: run(G)), G
+    for _ in range(max(1, warmup // per)):
+        fn()
     barrier_sync(world)
     t0 = time.perf_counter()
-    run(args.steps)
+    for _ in range(steps // per):
+        fn()
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    value = world * args.steps * BATCH / dt
-    prof = profile_kernels(model, lambda: run(min(args.steps, 50)))
-    # dominant = Adam over the 4,291,632 trainables: p,m,v read+write, g read = 7 x 4 B
+    value = world * steps * BATCH / dt
+    prof = profile_kernels(model, lambda: run(min(steps, 32)))
+    # dominant HBM kernel: fused Adam + re-pack over the 4,291,632 trainables:
+    # p, m, v read+write, g read (7 x 4 B) + Wf, Wd written (2 x 4 B per weight element)
     n_params = sum(n for _, n, k, _ in model.param_table if k == 0)
-    cnt, avg_us, _, _ = prof["adam"]
-    byts = 7 * 4 * n_params
+    n_w = sum(n for nm, n, k, _ in model.param_table if k == 0 and nm.split("/")[-1][0] == "w")
+    cnt, avg_us, _, _ = prof["adam_pack"]
+    byts = 7 * 4 * n_params + 2 * 4 * n_w
     achieved = byts / (avg_us * 1e-6) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": args.traffic, "kernel": "k_adam",
-            "bytes_per_launch": byts, "avg_us": round(avg_us, 3),
-            "per_kernel_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _committed_traffic("k_adam_pack"),
+            "kernel": "k_adam_pack", "bytes_per_launch": byts, "avg_us": round(avg_us, 3),
+            "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
     model.close()
-    return value, dt, roof
+    return value, dt, roof, ("graph" if use_graph else "eager")
 
 
 def main():
@@ -267,19 +294,32 @@ def main():
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
+    ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
     rank, world, local = setup_dist()
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    train = None
     if args.mode == "infer":
         value, dt, roof = bench_infer(args, rank, world)
         workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
                     "%d stream(s)" % args.streams)
+        if args.train_steps > 0:   # cfg3 beside the headline, same ranks (data parallel)
+            try:
+                tv, tdt, troof, tmode = bench_train(args, rank, world, steps=args.train_steps, warmup=64)
+                train = {"workload": "cfg3 train step (fwd+bwd+TF1 Adam), batch 64/GPU, keep 0.5, dp%d" % world,
+                         "value": round(tv, 1), "unit": "poses/s", "steps": args.train_steps,
+                         "ms_per_step": round(1000.0 * tdt / args.train_steps, 5), "mode": tmode,
+                         "roofline": troof}
+            except Exception as exc:  # report, never lose the headline line
+                train = {"error": repr(exc)[:300]}
     else:
-        value, dt, roof = bench_train(args, rank, world)
-        workload = "cfg3 train step: L=1024, 2 residual blocks, BN, dropout keep 0.5, batch 64/GPU, TF1 Adam"
+        value, dt, roof, tmode = bench_train(args, rank, world)
+        workload = ("cfg3 train step: L=1024, 2 residual blocks, BN, dropout keep 0.5, batch 64/GPU, TF1 Adam "
+                    "(%s)" % tmode)
     if rank == 0:
         cpu = None if args.no_cpu else cpu_baseline(args.mode, args.cpu_seconds)
         line = {"metric": "poses/sec at batch 64 (H3.6M 16-joint)", "value": round(value, 1), "unit": "poses/s",
@@ -289,6 +329,8 @@ def main():
                 "config": {"workload": workload, "global_batch": BATCH * world, "linear_size": L,
                            "num_layers": NBLK, "parallelism": "dp%d" % world},
                 "roofline": roof, "cpu_baseline": cpu}
+        if train is not None:
+            line["train"] = train
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

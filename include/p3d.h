@@ -34,6 +34,9 @@ extern "C" {
 #define P3D_ERR_STATE 3    /* call out of order (e.g. backward before fwd)   */
 #define P3D_ERR_NOTFOUND 4 /* unknown parameter name                         */
 
+/* p3d_forward ctr value meaning "use the device-resident global_step" (graph-capturable) */
+#define P3D_CTR_GLOBAL_STEP 0xFFFFFFFFFFFFFFFFull
+
 #define P3D_DTYPE_F32 0
 #define P3D_DTYPE_BF16 1   /* bf16 weights/activations, fp32 accumulate + BN */
 
@@ -113,11 +116,15 @@ int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stream);
 /* One TF1 ApplyAdam over all trainables (linear_model.py:137,145):
  *   alpha = lr*sqrt(1-beta2_power)/(1-beta1_power); m += (g-m)(1-b1);
  *   v += (g^2-v)(1-b2); w -= (m*alpha)/(sqrt(v)+eps)
- * lr is the already-decayed rate (tf.train.exponential_decay is host-side:
- * lr0 * 0.96^(global_step/1e5)).  beta powers advance and global_step += 1. */
+ * then global_step += 1 and the beta powers advance.  The step state lives on the
+ * device.  p3d_adam_step takes the already-decayed lr; p3d_adam_step_decay computes
+ * tf.train.exponential_decay (lr0 * rate^(global_step/steps), linear_model.py:88-90)
+ * on the device, so a whole training step can be captured in a HIP graph. */
 int p3d_adam_step(p3d_model* m, float lr, void* stream);
+int p3d_adam_step_decay(p3d_model* m, float lr0, float decay_steps, float decay_rate, void* stream);
 
-/* Adam bookkeeping (for checkpoints): global_step and beta1/beta2 powers. */
+/* Adam bookkeeping (for checkpoints): global_step and beta1/beta2 powers.  Both
+ * synchronise the device (the state is device-resident). */
 int p3d_get_step(const p3d_model* m, int64_t* global_step, float* beta1_power, float* beta2_power);
 int p3d_set_step(p3d_model* m, int64_t global_step, float beta1_power, float beta2_power);
 
