@@ -14,6 +14,7 @@
 //   k_mpjpe      fused un-normalize + per-joint L2 (fp64).   predict_3dpose.py:399-430
 //   k_dot_*      per-tensor reductions for --max_norm (||W||^2, <G,W>).
 #include "p3d_kernels.h"
+#include "p3d_bf16.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -679,6 +680,8 @@ struct Layer {
   int64_t w, b, gamma = -1, beta = -1;  // offsets in params
   int64_t mmean = -1, mvar = -1;        // offsets in moving
   int64_t wf, wd;                       // offsets in the packed-weight buffer
+  int64_t wbf = -1;                     // bf16 models: offset (bf16 units) of packed Wt
+  int64_t aff = -1;                     // bf16 models: offset of [inv | shift] (2N floats)
   int widx;                             // weight index (max-norm tables)
   int site;                             // dropout site; -1 for the output layer
   bool bn, relu;
@@ -697,6 +700,11 @@ struct p3d_model {
   float* wpk = nullptr;       // packed weights (Wf, Wd per layer)
   float* ws = nullptr;        // activation workspace
   float* scratch = nullptr;   // reductions (max-norm)
+  // bf16 inference models (cfg5)
+  unsigned short* wbf = nullptr;    // packed bf16 weights
+  float* aff = nullptr;             // BN-eval affine per BN layer
+  unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
+  int64_t Mpad128 = 0;
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
@@ -748,6 +756,9 @@ void free_all(p3d_model* m) {
   if (m->ws) (void)hipFree(m->ws);
   if (m->scratch) (void)hipFree(m->scratch);
   if (m->dstate) (void)hipFree(m->dstate);
+  if (m->wbf) (void)hipFree(m->wbf);
+  if (m->aff) (void)hipFree(m->aff);
+  if (m->abf) (void)hipFree(m->abf);
 }
 }  // namespace
 
@@ -763,7 +774,9 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     return fail(P3D_ERR_ARG, "input_size must be a positive multiple of 16");
   if (c.output_size <= 0) return fail(P3D_ERR_ARG, "output_size must be positive");
   if (c.max_batch <= 0) return fail(P3D_ERR_ARG, "max_batch must be positive");
-  if (c.dtype != P3D_DTYPE_F32) return fail(P3D_ERR_ARG, "only P3D_DTYPE_F32 models in this build");
+  if (c.dtype != P3D_DTYPE_F32 && c.dtype != P3D_DTYPE_BF16) return fail(P3D_ERR_ARG, "dtype must be F32 or BF16");
+  if (c.dtype == P3D_DTYPE_BF16 && (c.linear_size % 128 != 0 || c.input_size % 32 != 0))
+    return fail(P3D_ERR_ARG, "bf16 models need linear_size % 128 == 0 and input_size % 32 == 0");
   p3d_model* m = new p3d_model();
   m->cfg = c;
   const int L = c.linear_size;
@@ -924,6 +937,21 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
         return cleanup(e);
     }
   }
+  if (c.dtype == P3D_DTYPE_BF16) {
+    int64_t nbf = 0, naff = 0;
+    for (auto& ly : m->layers) {
+      const int NP = (ly.N + 15) / 16 * 16;
+      ly.wbf = nbf; nbf += pad64((int64_t)NP * ly.K);
+      if (ly.bn) { ly.aff = naff; naff += 2 * pad64(ly.N); }
+    }
+    m->Mpad128 = (c.max_batch + 127) / 128 * 128;
+    const int64_t slab = m->Mpad128 * L;  // bf16 elements per activation slab
+    if ((e = hipMalloc(&m->wbf, nbf * 2)) != hipSuccess) return cleanup(e);
+    if ((e = hipMemset(m->wbf, 0, nbf * 2)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&m->aff, (naff + 64) * 4)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&m->abf, (int64_t)(nl + 1) * slab * 2)) != hipSuccess) return cleanup(e);
+    if ((e = hipMemset(m->abf, 0, (int64_t)(nl + 1) * slab * 2)) != hipSuccess) return cleanup(e);
+  }
   *out = m;
   return P3D_OK;
 }
@@ -981,6 +1009,20 @@ extern "C" int p3d_flat_ptr(p3d_model* m, int32_t which, void** dptr, int64_t* n
 }
 
 static int refresh_derived(p3d_model* m, hipStream_t st) {
+  if (m->cfg.dtype == P3D_DTYPE_BF16) {
+    for (const Layer& ly : m->layers) {
+      const int NP = (ly.N + 15) / 16 * 16;
+      const int64_t items = (int64_t)(NP / 16) * (ly.K / 32) * 64;
+      k_pack_bf16<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(m->flat[0] + ly.w, ly.K, ly.N, m->wbf + ly.wbf);
+      LAUNCH_CHECK("k_pack_bf16");
+      if (ly.bn) {
+        k_bn_affine<<<(ly.N + 255) / 256, 256, 0, st>>>(m->flat[0] + ly.gamma, m->flat[0] + ly.beta,
+                                                        m->moving + ly.mmean, m->moving + ly.mvar, m->cfg.bn_eps,
+                                                        ly.N, m->aff + ly.aff, m->aff + ly.aff + ly.N);
+        LAUNCH_CHECK("k_bn_affine");
+      }
+    }
+  }
   const int64_t n4 = m->pt.begin[m->pt.n];
   {
     ProfScope ps(m, "pack", st);
@@ -1030,6 +1072,63 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
+  const p3d_cfg& c = m->cfg;
+  const int64_t slab = m->Mpad128 * c.linear_size;
+  const int nl = (int)m->layers.size();
+  const Layer& ly = m->layers[l];
+  GemmBf16Args a{};
+  a.A = l == 0 ? m->abf + (int64_t)nl * slab : m->abf + (int64_t)(l - 1) * slab;
+  a.Bt = m->wbf + ly.wbf; a.Y = m->abf + (int64_t)l * slab;
+  a.M = Mp; a.N = ly.N; a.K = ly.K;
+  a.epi.bias = m->flat[0] + ly.b;
+  a.epi.inv = ly.bn ? m->aff + ly.aff : nullptr;
+  a.epi.shift = ly.bn ? m->aff + ly.aff + ly.N : nullptr;
+  a.epi.relu = 1;
+  const bool second = (l >= 1 && ((l - 1) % 2 == 1));
+  a.res = (c.residual && second) ? m->abf + (int64_t)(l - 2) * slab : nullptr;
+  const unsigned grid = (unsigned)((Mp / 128) * (ly.N / 128));
+  {
+    ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden", st);
+    if (l == 0) k_gemm_bf16<32><<<grid, 256, 0, st>>>(a);
+    else k_gemm_bf16<64><<<grid, 256, 0, st>>>(a);
+  }
+  LAUNCH_CHECK("k_gemm_bf16");
+  return P3D_OK;
+}
+
+// cfg5 path: x -> bf16 packed, input layer and every hidden layer through the LDS-staged
+// bf16 GEMM (fused bias/BN/ReLU/residual, bf16 out), output layer register-direct (fp32 out).
+static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipStream_t st) {
+  const p3d_cfg& c = m->cfg;
+  const int L = c.linear_size;
+  const int Mp = (int)((B + 127) / 128 * 128);
+  const int64_t slab = m->Mpad128 * L;
+  const int nl = (int)m->layers.size();
+  unsigned short* xs = m->abf + (int64_t)nl * slab;
+  {
+    const int64_t items = (int64_t)(Mp / 16) * (c.input_size / 32) * 64;
+    ProfScope ps(m, "bf16_x", st);
+    k_x_to_bf16<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(x, (int)B, c.input_size, xs, Mp);
+  }
+  LAUNCH_CHECK("k_x_to_bf16");
+  for (int l = 0; l < nl - 1; ++l) {
+    const int rc = launch_bf16_layer(m, l, Mp, st);
+    if (rc) return rc;
+  }
+  const unsigned short* in = m->abf + (int64_t)(nl - 2) * slab;
+  const Layer& lo = m->layers[nl - 1];
+  SmallBf16Args o{};
+  o.A = in; o.Bt = m->wbf + lo.wbf; o.M = (int)B; o.N = lo.N; o.K = lo.K;
+  o.bias = m->flat[0] + lo.b; o.Y = y; o.ldy = lo.N;
+  {
+    ProfScope ps(m, "bf16_out", st);
+    k_out_bf16<16><<<dim3((lo.N + 15) / 16, Mp / 16), 1024, 0, st>>>(o);
+  }
+  LAUNCH_CHECK("k_out_bf16");
+  return P3D_OK;
+}
+
 extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
                               float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row,
                               void* stream) {
@@ -1046,6 +1145,12 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
   if (!(keep_prob > 0.f && keep_prob <= 1.f)) return fail(P3D_ERR_ARG, "keep_prob must be in (0, 1]");
   if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_forward: x must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
+  if (c.dtype == P3D_DTYPE_BF16) {
+    if (training) return fail(P3D_ERR_ARG, "p3d_forward: bf16 models are inference-only");
+    if (keep_prob < 1.0f) return fail(P3D_ERR_ARG, "p3d_forward: bf16 models do not implement dropout");
+    if (ws_row != 0) return fail(P3D_ERR_ARG, "p3d_forward_ex: bf16 models use workspace row 0");
+    return forward_bf16(m, x, B, y, st);
+  }
   const float decay = 1.0f - c.bn_momentum;
   const int nl = (int)m->layers.size();
   const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
@@ -1105,6 +1210,14 @@ extern "C" int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t re
   const int nl = (int)m->layers.size();
   if (layer < 1 || layer > nl - 2) return fail(P3D_ERR_ARG, "p3d_time_layer: layer must be a hidden layer");
   if (B <= 0 || B > c.max_batch) return fail(P3D_ERR_ARG, "p3d_time_layer: bad batch");
+  if (c.dtype == P3D_DTYPE_BF16) {
+    const int Mp = (int)((B + 127) / 128 * 128);
+    for (int r = 0; r < reps; ++r) {
+      const int rc = launch_bf16_layer(m, layer, Mp, (hipStream_t)stream);
+      if (rc) return rc;
+    }
+    return P3D_OK;
+  }
   const Layer& ly = m->layers[layer];
   FwdArgs a{};
   a.X = m->act[layer - 1]; a.Wf = m->wpk + ly.wf; a.bias = m->flat[0] + ly.b;

@@ -147,8 +147,10 @@ class LinearModel(object):
         if not torch.cuda.is_available():
             raise _p3d.P3DError("LinearModel needs a ROCm GPU (torch.cuda.is_available() is False); "
                                 "the HIP path has no CPU fallback")
-        if dtype is not None and str(dtype).split(".")[-1] not in ("float32", "tf.float32"):
-            raise ValueError("this build implements the fp32 graph only (got dtype=%r)" % (dtype,))
+        dname = None if dtype is None else str(dtype).split(".")[-1]
+        if dname not in (None, "float32", "bfloat16"):
+            raise ValueError("dtype must be float32 or bfloat16 (got %r)" % (dtype,))
+        self.bf16 = dname == "bfloat16"   # cfg5: bf16 weights/activations, fp32 accumulate, inference only
         self.torch = torch
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.HUMAN_2D_SIZE = HUMAN_2D_SIZE
@@ -167,7 +169,8 @@ class LinearModel(object):
         self.max_batch = int(max_batch or max(self.batch_size, 64))
 
         cfg = _p3d.P3DCfg(self.linear_size, self.num_layers, int(self.residual), int(self.batch_norm),
-                          int(self.max_norm), self.input_size, self.output_size, _p3d.P3D_DTYPE_F32,
+                          int(self.max_norm), self.input_size, self.output_size,
+                          _p3d.P3D_DTYPE_BF16 if self.bf16 else _p3d.P3D_DTYPE_F32,
                           self.max_batch, 1e-3, 0.99)
         h = _p3d.c_void_p()
         with torch.cuda.device(self.device):

@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (AMD's 5 PF figure is 2:1 sparse)
 
 L, NBLK, IN, OUT, BATCH = 1024, 2, 32, 48, 64
 
@@ -284,12 +285,72 @@ def bench_train(args, rank, world, steps=None, warmup=None):
     return value, dt, roof, ("graph" if use_graph else "eager")
 
 
+def bench_stress(args, rank, world):
+    """cfg5: L=4096, 4 residual blocks, bf16 weights/activations with fp32 accumulate and
+    fp32 BN, batch 1024, inference.  One step = one forward of one batch of 1024 poses."""
+    import torch
+    import _p3d
+    import linear_model
+    Ls, Ns, Bs = 4096, 4, 1024
+    model = linear_model.LinearModel(Ls, Ns, True, True, False, Bs, 1e-3, "/tmp/p3d_bench", dtype="bfloat16",
+                                     seed=7, max_batch=Bs, data_parallel=False)
+    rng = np.random.default_rng(2)
+    bn = {}
+    for name, numel, kind, _ in model.param_table:
+        if name.endswith("/gamma"):
+            bn[name] = rng.uniform(0.5, 1.5, numel)
+        elif name.endswith("/beta") or name.endswith("/moving_mean"):
+            bn[name] = rng.normal(0.0, 0.1, numel)
+        elif name.endswith("/moving_variance"):
+            bn[name] = rng.uniform(0.5, 2.0, numel)
+    model.set_weights(bn)
+    G = 8
+    X = torch.from_numpy(np.random.default_rng(300 + rank).standard_normal((G, Bs, IN)).astype(np.float32)).cuda()
+    Y = torch.empty((G, Bs, OUT), dtype=torch.float32, device="cuda")
+
+    def run(k):
+        for i in range(k):
+            model.forward_device(X[i % G], False, 1.0, out=Y[i % G])
+
+    run(G)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        run(G)
+    steps = max(G, args.steps // G * G)
+    for _ in range(max(1, args.warmup // G)):
+        graph.replay()
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(steps // G):
+        graph.replay()
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    value = world * steps * Bs / dt
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, Bs, 5, model.stream()), "p3d_time_layer")
+    e0.record()
+    _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, Bs, reps, model.stream()), "p3d_time_layer")
+    e1.record()
+    torch.cuda.synchronize()
+    avg_us = 1000.0 * e0.elapsed_time(e1) / reps
+    flop = 2.0 * Bs * Ls * Ls
+    achieved = flop / (avg_us * 1e-6) / 1e12
+    roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16<64>"),
+            "kernel": "k_gemm_bf16<64> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
+            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps}
+    model.close()
+    return value, dt, roof, steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--mode", choices=["infer", "train"], default="infer")
+    ap.add_argument("--mode", choices=["infer", "train", "stress"], default="infer")
     ap.add_argument("--graph-steps", type=int, default=48)
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -316,16 +377,23 @@ def main():
                          "roofline": troof}
             except Exception as exc:  # report, never lose the headline line
                 train = {"error": repr(exc)[:300]}
+    elif args.mode == "stress":
+        value, dt, roof, args.steps = bench_stress(args, rank, world)
+        workload = "cfg5 inference: L=4096, 4 residual blocks, BN(eval), batch 1024 per step, bf16/fp32-acc"
     else:
         value, dt, roof, tmode = bench_train(args, rank, world)
         workload = ("cfg3 train step: L=1024, 2 residual blocks, BN, dropout keep 0.5, batch 64/GPU, TF1 Adam "
                     "(%s)" % tmode)
     if rank == 0:
         cpu = None if args.no_cpu else cpu_baseline(args.mode, args.cpu_seconds)
-        line = {"metric": "poses/sec at batch 64 (H3.6M 16-joint)", "value": round(value, 1), "unit": "poses/s",
+        if args.mode == "stress":
+            cpu = None
+        line = {"metric": "poses/sec at batch 64 (H3.6M 16-joint)" if args.mode != "stress" else
+                "poses/sec at batch 1024 (cfg5 bf16 stress)", "value": round(value, 1), "unit": "poses/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(1000.0 * dt / args.steps, 5), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.mode == "stress" else "f32",
+                "data": "synthetic",
                 "config": {"workload": workload, "global_batch": BATCH * world, "linear_size": L,
                            "num_layers": NBLK, "parallelism": "dp%d" % world},
                 "roofline": roof, "cpu_baseline": cpu}

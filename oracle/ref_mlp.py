@@ -454,3 +454,45 @@ def eval_step(state: State, x, t, dt=np.float64):
     out, _ = forward(state, x, False, 1.0, 0, 0, 0, dt)
     loss, _ = mse(out, t, dt)
     return loss, out
+
+
+# --------------------------------------------------------------------------------------
+# bf16 inference emulation (cfg5: bf16 weights/activations, fp32 accumulate + BN)
+# --------------------------------------------------------------------------------------
+
+
+def bf16_round(a):
+    """Round to the nearest bf16 (ties to even), returned as float32."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)) << np.uint64(16)
+    return r.astype(np.uint32).view(np.float32)
+
+
+def forward_bf16(state: State, x, acc=np.float64):
+    """Inference forward of the bf16 path: x and every weight rounded to bf16, products
+    accumulated in ``acc``, epilogue (bias, BN eval, ReLU, residual) in fp32, each hidden
+    activation rounded to bf16 when stored; output layer stays fp32."""
+    cfg = state.cfg
+    P = state.params
+    f32 = np.float32
+
+    def layer(a, wname, bname, bn, res=None):
+        z = (a.astype(acc) @ bf16_round(P[wname]).astype(acc)).astype(f32) + P[bname]
+        if bn is not None:
+            inv = (f32(1.0) / np.sqrt(state.moving[bn + "/moving_variance"] + f32(cfg.bn_eps))) * P[bn + "/gamma"]
+            z = z * inv + (P[bn + "/beta"] - state.moving[bn + "/moving_mean"] * inv)
+        y = np.maximum(z, f32(0.0))
+        if res is not None:
+            y = y + res
+        return bf16_round(y)
+
+    bns = bn_names(cfg)
+    h = layer(bf16_round(np.asarray(x, np.float32)), "linear_model/w1", "linear_model/b1", bns[0] if bns else None)
+    for i in range(cfg.num_layers):
+        s = "linear_model/two_linear_%d/" % i
+        xin = h
+        a = layer(xin, s + "w2_%d" % i, s + "b2_%d" % i, bns[1 + 2 * i] if bns else None)
+        h = layer(a, s + "w3_%d" % i, s + "b3_%d" % i, bns[2 + 2 * i] if bns else None,
+                  res=xin if cfg.residual else None)
+    out = (h.astype(acc) @ bf16_round(P["linear_model/w4"]).astype(acc)).astype(np.float32) + P["linear_model/b4"]
+    return out

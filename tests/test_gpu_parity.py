@@ -169,3 +169,28 @@ def test_bad_shapes_raise():
     with pytest.raises(ValueError):
         m.forward_device(torch.zeros((4096, 32), device="cuda"))
     m.close()
+
+
+@pytest.mark.parametrize("L,N,B", [(256, 2, 128), (512, 1, 200), (4096, 4, 1024)])
+def test_bf16_inference_matches_emulated_oracle(L, N, B):
+    """cfg5 path (bf16 weights/activations, fp32 accumulate) vs the oracle's bf16 emulation.
+    Tolerance: 2% of the output range (one bf16 ulp is 0.4%; a flipped rounding of a hidden
+    activation propagates), and 2e-3 mean absolute deviation."""
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
+    m = linear_model.LinearModel(L, N, True, True, False, B, 1e-3, "/tmp/p3d_test", dtype="bfloat16",
+                                 seed=3, max_batch=B)
+    m.set_weights({**st.params, **st.moving})
+    x = np.random.default_rng(B).standard_normal((B, 32)).astype(np.float32)
+    y = m.forward_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    ref = ref_mlp.forward_bf16(st, x, acc=np.float32 if L >= 4096 else np.float64)
+    scale = np.abs(ref).max()
+    err = np.abs(y - ref)
+    assert err.max() <= 0.02 * scale, (err.max(), scale)
+    assert err.mean() <= 2e-3 * scale, (err.mean(), scale)
+    # and it is close to the fp32 model (bf16 is an approximation of cfg2's arithmetic)
+    ref32, _ = ref_mlp.forward(st, x, False)
+    assert np.abs(y - ref32).mean() <= 0.05 * np.abs(ref32).mean()
+    with pytest.raises(ValueError):
+        m.forward_device(torch.from_numpy(x).cuda(), training=True)
+    m.close()
