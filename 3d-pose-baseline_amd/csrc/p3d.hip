@@ -18,6 +18,7 @@
 #include "../../include/p3d.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -705,6 +706,7 @@ struct p3d_model {
   float* aff = nullptr;             // BN-eval affine per BN layer
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
+  int bf16_stages = 4;              // LDS ring depth of the hidden bf16 GEMM (P3D_BF16_STAGES)
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
@@ -945,6 +947,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
       if (ly.bn) { ly.aff = naff; naff += 2 * pad64(ly.N); }
     }
     m->Mpad128 = (c.max_batch + 127) / 128 * 128;
+    if (const char* ev = getenv("P3D_BF16_STAGES")) m->bf16_stages = atoi(ev);
     const int64_t slab = m->Mpad128 * L;  // bf16 elements per activation slab
     if ((e = hipMalloc(&m->wbf, nbf * 2)) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->wbf, 0, nbf * 2)) != hipSuccess) return cleanup(e);
@@ -1090,8 +1093,10 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
   const unsigned grid = (unsigned)((Mp / 128) * (ly.N / 128));
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden", st);
-    if (l == 0) k_gemm_bf16<32><<<grid, 256, 0, st>>>(a);
-    else k_gemm_bf16<64><<<grid, 256, 0, st>>>(a);
+    if (l == 0) k_gemm_bf16<32, 2><<<grid, 256, 0, st>>>(a);
+    else if (m->bf16_stages == 2) k_gemm_bf16<64, 2><<<grid, 256, 0, st>>>(a);
+    else if (m->bf16_stages == 3) k_gemm_bf16<64, 3><<<grid, 256, 0, st>>>(a);
+    else k_gemm_bf16<64, 4><<<grid, 256, 0, st>>>(a);
   }
   LAUNCH_CHECK("k_gemm_bf16");
   return P3D_OK;
