@@ -728,6 +728,10 @@ struct p3d_model {
   uint64_t seed = 0, ctr = 0;
   int64_t row_off = 0;
   const int64_t* ctr_dev = nullptr;   // cached training-forward counter source
+  // waves per inference workgroup (P3D_INFER_WK = 8 | 16).  8 waves x 94 VGPRs lets two
+  // workgroups co-reside per CU, so independent batches on different streams overlap
+  // (tools/streams_sweep2.py: 4 streams 5.6 M poses/s vs 4.9 M with 16-wave workgroups).
+  int infer_wk = 8;
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -921,6 +925,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   m->dout[1] = cur; cur += pad64(Bp * L);
   const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
+  if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev) == 8 ? 8 : 16;
   {
     StepState s0{};
     s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
@@ -1048,17 +1053,18 @@ extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
 
 // ---- launch helpers ------------------------------------------------------------------
 // Inference: 16x16 output tile per workgroup (grid 64 x 4 = 256 WGs for the 1024-wide
-// layers at B = 64), 16 waves split the contraction 16 ways (every operand load issued up
-// front).  BN-train: one workgroup owns all 64 rows of its 16 columns (batch statistics
+// layers at B = 64), 8 (or 16) waves split the contraction (every operand load of a wave
+// issued up front).  BN-train: one workgroup owns all 64 rows of its 16 columns (batch statistics
 // are workgroup-local), 8 waves split the contraction.
 template <bool APK, bool YPK, int KIND>
-static void launch_fwd_k(const FwdArgs& a, bool whole_batch, hipStream_t st) {
+static void launch_fwd_k(const FwdArgs& a, bool whole_batch, int wk, hipStream_t st) {
   const int gx = (a.N + 15) / 16;
   if (whole_batch) {
     k_fwd<4, 8, 8, 2, APK, YPK, KIND><<<dim3(gx, 1), 512, 0, st>>>(a);
   } else {
     const int gy = (a.M + 15) / 16;
-    k_fwd<1, 16, 4, 2, APK, YPK, KIND><<<dim3(gx, gy), 1024, 0, st>>>(a);
+    if (wk == 8) k_fwd<1, 8, 8, 2, APK, YPK, KIND><<<dim3(gx, gy), 512, 0, st>>>(a);
+    else k_fwd<1, 16, 4, 2, APK, YPK, KIND><<<dim3(gx, gy), 1024, 0, st>>>(a);
   }
 }
 
@@ -1066,9 +1072,9 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind], st);
-  if (kind == 0) launch_fwd_k<false, true, 0>(a, whole_batch, st);
-  else if (kind == 1) launch_fwd_k<true, true, 1>(a, whole_batch, st);
-  else launch_fwd_k<true, false, 2>(a, whole_batch, st);
+  if (kind == 0) launch_fwd_k<false, true, 0>(a, whole_batch, m->infer_wk, st);
+  else if (kind == 1) launch_fwd_k<true, true, 1>(a, whole_batch, m->infer_wk, st);
+  else launch_fwd_k<true, false, 2>(a, whole_batch, m->infer_wk, st);
   LAUNCH_CHECK("k_fwd");
   return P3D_OK;
 }

@@ -149,10 +149,11 @@ def cpu_baseline(mode, seconds=12.0):
 
 
 def bench_infer(args, rank, world):
-    """K forward steps of one 64-pose batch each.  S streams each own a disjoint slice of
-    the workspace (p3d_forward_ex ws_row) so independent batches overlap on the GPU; every
-    batch still runs its own six layer kernels at M = 64 and is bit-identical to a
-    sequential p3d_forward."""
+    """K forward steps of one 64-pose batch each.  S streams (one per hardware queue) each
+    replay their own HIP graph of G/S steps over a disjoint workspace slot
+    (p3d_forward_ex ws_row), so independent batches overlap on the GPU; every batch still
+    runs its own six layer kernels at M = 64 and is bit-identical to a sequential
+    p3d_forward.  The single-stream rate is measured too (``single_stream``)."""
     import torch
     S = args.streams
     model, _ = make_model(data_parallel=False, max_batch=BATCH * S)
@@ -162,42 +163,61 @@ def bench_infer(args, rank, world):
     rng = np.random.default_rng(100 + rank)
     X = torch.from_numpy(rng.standard_normal((G, BATCH, IN)).astype(np.float32)).cuda()
     Y = torch.empty((G, BATCH, OUT), dtype=torch.float32, device="cuda")
-    streams = [torch.cuda.Stream() for _ in range(S)]
 
     def steps_eager(k, base=0):
         for i in range(k):
             model.forward_device(X[(base + i) % G], False, 1.0, out=Y[(base + i) % G], ctr=0)
 
-    def steps_multi():
-        cur = torch.cuda.current_stream()
-        for st in streams:
-            st.wait_stream(cur)
-        for j, st in enumerate(streams):
-            with torch.cuda.stream(st):
-                for i in range(j, G, S):
-                    model.forward_device(X[i], False, 1.0, out=Y[i], ctr=0, ws_row=BATCH * j)
-        for st in streams:
-            cur.wait_stream(st)
-
-    s0 = torch.cuda.Stream()
-    s0.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s0):
-        steps_multi()
-    torch.cuda.current_stream().wait_stream(s0)
+    # HIP binds a stream to one of GPU_MAX_HW_QUEUES (=4) hardware queues on first use,
+    # round robin; the first pool streams share queues with torch's own, so one round of
+    # streams is touched first and the batch streams land on 4 distinct idle queues
+    # (tools/streams_probe.py: 3.8 -> 5.6 M poses/s at 4 streams).
+    spare = [torch.cuda.Stream() for _ in range(4)]
+    for st in spare:
+        with torch.cuda.stream(st):
+            torch.zeros(16, device="cuda").add_(1)
     torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        steps_multi()
-    reps_w = max(1, args.warmup // G)
-    for _ in range(reps_w):
-        graph.replay()
-    barrier_sync(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps // G):
-        graph.replay()
-    barrier_sync(world)
-    dt = max_over_ranks(time.perf_counter() - t0, world)
+
+    def capture(nstreams):
+        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+        per = G // nstreams
+        graphs = []
+        for j, st in enumerate(streams):
+            def body(j=j):
+                for i in range(per):
+                    model.forward_device(X[j * per + i], False, 1.0, out=Y[j * per + i], ctr=0,
+                                         ws_row=BATCH * j)
+            with torch.cuda.stream(st):
+                body()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                body()
+            graphs.append(g)
+        torch.cuda.synchronize()
+
+        def replay():
+            for j, st in enumerate(streams):
+                with torch.cuda.stream(st):
+                    graphs[j].replay()
+        return replay
+
+    def timed(fn, steps):
+        for _ in range(max(1, args.warmup // G)):
+            fn()
+        barrier_sync(world)
+        t0 = time.perf_counter()
+        for _ in range(steps // G):
+            fn()
+        barrier_sync(world)
+        return max_over_ranks(time.perf_counter() - t0, world)
+
+    dt = timed(capture(S), args.steps)
     value = world * args.steps * BATCH / dt
+    single = None
+    if S > 1:
+        dt1 = timed(capture(1), args.steps)
+        single = {"value": round(world * args.steps * BATCH / dt1, 1), "ms_per_step": round(1000.0 * dt1 / args.steps, 5)}
 
     # dominant kernel, timed live: 200 back-to-back launches of the first hidden layer
     # (k_fwd<...,1>) bracketed by one hipEvent pair on the launching stream -> average
@@ -214,14 +234,14 @@ def bench_infer(args, rank, world):
     prof = profile_kernels(model, lambda: steps_eager(min(args.steps, 100)))
     flop = 2.0 * BATCH * L * L          # one hidden-layer launch: [64,1024] x [1024,1024]
     achieved = flop / (avg_us * 1e-6) / 1e12
-    traffic = args.traffic if args.traffic is not None else _committed_traffic("k_fwd<1, 16, 4, 2, true, true, 1>")
+    traffic = args.traffic if args.traffic is not None else _committed_traffic("k_fwd<1, 8, 8, 2, true, true, 1>")
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-            "kernel": "k_fwd<1,16,4,2,true,true,1> (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
+            "kernel": "k_fwd<1,8,8,2,true,true,1> (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
             "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
     model.close()
-    return value, dt, roof
+    return value, dt, roof, single
 
 
 def bench_train(args, rank, world, steps=None, warmup=None):
@@ -351,7 +371,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--mode", choices=["infer", "train", "stress"], default="infer")
-    ap.add_argument("--graph-steps", type=int, default=48)
+    ap.add_argument("--graph-steps", type=int, default=240)
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -363,9 +383,9 @@ def main():
     rank, world, local = setup_dist()
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    train = None
+    train = single = None
     if args.mode == "infer":
-        value, dt, roof = bench_infer(args, rank, world)
+        value, dt, roof, single = bench_infer(args, rank, world)
         workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
                     "%d stream(s)" % args.streams)
         if args.train_steps > 0:   # cfg3 beside the headline, same ranks (data parallel)
@@ -397,6 +417,8 @@ def main():
                 "config": {"workload": workload, "global_batch": BATCH * world, "linear_size": L,
                            "num_layers": NBLK, "parallelism": "dp%d" % world},
                 "roofline": roof, "cpu_baseline": cpu}
+        if single is not None:
+            line["single_stream"] = single
         if train is not None:
             line["train"] = train
         print(json.dumps(line), flush=True)
