@@ -13,6 +13,7 @@
 //   k_mse        loss = mean((y-t)^2), dy = 2(y-t)/(B*D).     linear_model.py:129
 //   k_mpjpe      fused un-normalize + per-joint L2 (fp64).   predict_3dpose.py:399-430
 //   k_dot_*      per-tensor reductions for --max_norm (||W||^2, <G,W>).
+#include <hip/hip_ext.h>
 #include "p3d_kernels.h"
 #include "p3d_bf16.h"
 #include "../../include/p3d.h"
@@ -740,19 +741,29 @@ struct p3d_model {
 };
 
 namespace {
-struct ProfScope {  // brackets one kernel launch with an event pair when profiling
-  p3d_model* m; hipStream_t st; bool on;
-  ProfScope(p3d_model* m_, const char* tag, hipStream_t st_) : m(m_), st(st_), on(false) {
+struct ProfScope {  // times one kernel launch when profiling (p3d_profile_start/stop)
+  p3d_model* m; hipEvent_t e0, e1; bool on;
+  ProfScope(p3d_model* m_, const char* tag) : m(m_), e0(nullptr), e1(nullptr), on(false) {
     if (m && m->prof && 2 * (m->ev_used + 1) <= m->ev.size()) {
       on = true;
       m->ev_tag[m->ev_used] = tag;
-      (void)hipEventRecord(m->ev[2 * m->ev_used], st);
+      e0 = m->ev[2 * m->ev_used];
+      e1 = m->ev[2 * m->ev_used + 1];
     }
   }
   ~ProfScope() {
-    if (on) { (void)hipEventRecord(m->ev[2 * m->ev_used + 1], st); ++m->ev_used; }
+    if (on) ++m->ev_used;
   }
 };
+
+// Launch `k`; under profiling the event pair is attached to the dispatch itself
+// (hipExtLaunchKernel start/stop events = the AQL packet's begin/end timestamps, the
+// same interval rocprofv3 --kernel-trace reports), not recorded as separate packets.
+template <typename F, typename... A>
+void go(const ProfScope& ps, F k, dim3 grid, dim3 block, hipStream_t st, A... args) {
+  if (ps.on) hipExtLaunchKernelGGL(k, grid, block, 0, st, ps.e0, ps.e1, 0, args...);
+  else k<<<grid, block, 0, st>>>(args...);
+}
 
 void free_all(p3d_model* m) {
   for (auto e : m->ev) (void)hipEventDestroy(e);
@@ -1033,8 +1044,8 @@ static int refresh_derived(p3d_model* m, hipStream_t st) {
   }
   const int64_t n4 = m->pt.begin[m->pt.n];
   {
-    ProfScope ps(m, "pack", st);
-    k_pack<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(m->flat[0], m->wpk, m->pt);
+    ProfScope ps(m, "pack");
+    go(ps, k_pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), st, (const float*)m->flat[0], m->wpk, m->pt);
   }
   LAUNCH_CHECK("k_pack");
   if (m->cfg.max_norm) {
@@ -1057,24 +1068,24 @@ extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
 // issued up front).  BN-train: one workgroup owns all 64 rows of its 16 columns (batch statistics
 // are workgroup-local), 8 waves split the contraction.
 template <bool APK, bool YPK, int KIND>
-static void launch_fwd_k(const FwdArgs& a, bool whole_batch, int wk, hipStream_t st) {
+static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch, int wk, hipStream_t st) {
   const int gx = (a.N + 15) / 16;
   if (whole_batch) {
-    k_fwd<4, 8, 8, 2, APK, YPK, KIND><<<dim3(gx, 1), 512, 0, st>>>(a);
+    go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
   } else {
     const int gy = (a.M + 15) / 16;
-    if (wk == 8) k_fwd<1, 8, 8, 2, APK, YPK, KIND><<<dim3(gx, gy), 512, 0, st>>>(a);
-    else k_fwd<1, 16, 4, 2, APK, YPK, KIND><<<dim3(gx, gy), 1024, 0, st>>>(a);
+    if (wk == 8) go(ps, k_fwd<1, 8, 8, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else go(ps, k_fwd<1, 16, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(1024), st, a);
   }
 }
 
 static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch, hipStream_t st) {
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
-  ProfScope ps(m, tags[whole_batch ? 1 : 0][kind], st);
-  if (kind == 0) launch_fwd_k<false, true, 0>(a, whole_batch, m->infer_wk, st);
-  else if (kind == 1) launch_fwd_k<true, true, 1>(a, whole_batch, m->infer_wk, st);
-  else launch_fwd_k<true, false, 2>(a, whole_batch, m->infer_wk, st);
+  ProfScope ps(m, tags[whole_batch ? 1 : 0][kind]);
+  if (kind == 0) launch_fwd_k<false, true, 0>(ps, a, whole_batch, m->infer_wk, st);
+  else if (kind == 1) launch_fwd_k<true, true, 1>(ps, a, whole_batch, m->infer_wk, st);
+  else launch_fwd_k<true, false, 2>(ps, a, whole_batch, m->infer_wk, st);
   LAUNCH_CHECK("k_fwd");
   return P3D_OK;
 }
@@ -1098,11 +1109,11 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
   a.res = (c.residual && second) ? m->abf + (int64_t)(l - 2) * slab : nullptr;
   const unsigned grid = (unsigned)((Mp / 128) * (ly.N / 128));
   {
-    ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden", st);
-    if (l == 0) k_gemm_bf16<32, 2><<<grid, 256, 0, st>>>(a);
-    else if (m->bf16_stages == 2) k_gemm_bf16<64, 2><<<grid, 256, 0, st>>>(a);
-    else if (m->bf16_stages == 3) k_gemm_bf16<64, 3><<<grid, 256, 0, st>>>(a);
-    else k_gemm_bf16<64, 4><<<grid, 256, 0, st>>>(a);
+    ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
+    if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 2) go(ps, k_gemm_bf16<64, 2>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 3) go(ps, k_gemm_bf16<64, 3>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_gemm_bf16<64, 4>, dim3(grid), dim3(256), st, a);
   }
   LAUNCH_CHECK("k_gemm_bf16");
   return P3D_OK;
@@ -1119,8 +1130,8 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
   unsigned short* xs = m->abf + (int64_t)nl * slab;
   {
     const int64_t items = (int64_t)(Mp / 16) * (c.input_size / 32) * 64;
-    ProfScope ps(m, "bf16_x", st);
-    k_x_to_bf16<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(x, (int)B, c.input_size, xs, Mp);
+    ProfScope ps(m, "bf16_x");
+    go(ps, k_x_to_bf16, dim3((unsigned)((items + 255) / 256)), dim3(256), st, x, (int)B, c.input_size, xs, Mp);
   }
   LAUNCH_CHECK("k_x_to_bf16");
   for (int l = 0; l < nl - 1; ++l) {
@@ -1133,8 +1144,8 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
   o.A = in; o.Bt = m->wbf + lo.wbf; o.M = (int)B; o.N = lo.N; o.K = lo.K;
   o.bias = m->flat[0] + lo.b; o.Y = y; o.ldy = lo.N;
   {
-    ProfScope ps(m, "bf16_out", st);
-    k_out_bf16<16><<<dim3((lo.N + 15) / 16, Mp / 16), 1024, 0, st>>>(o);
+    ProfScope ps(m, "bf16_out");
+    go(ps, k_out_bf16<16>, dim3((lo.N + 15) / 16, Mp / 16), dim3(1024), st, o);
   }
   LAUNCH_CHECK("k_out_bf16");
   return P3D_OK;
@@ -1258,8 +1269,8 @@ extern "C" int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, flo
 }
 
 static int launch_wgrad(p3d_model* m, const WgradArgs& a, hipStream_t st) {
-  ProfScope ps(m, "wgrad", st);
-  k_wgrad<<<dim3((a.N + 63) / 64, (a.K + 63) / 64), 256, 0, st>>>(a);
+  ProfScope ps(m, "wgrad");
+  go(ps, k_wgrad, dim3((a.N + 63) / 64, (a.K + 63) / 64), dim3(256), st, a);
   LAUNCH_CHECK("k_wgrad");
   return P3D_OK;
 }
@@ -1317,10 +1328,10 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     a.dz = m->dz[l - 1];
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
     {
-      ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden", st);
+      ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
       const dim3 grid((a.K + 15) / 16, 1);
-      if (dz_pk) k_dgrad<8, 8, 2, true, 1><<<grid, 512, 0, st>>>(a);
-      else k_dgrad<8, 8, 2, false, 2><<<grid, 512, 0, st>>>(a);
+      if (dz_pk) go(ps, k_dgrad<8, 8, 2, true, 1>, grid, dim3(512), st, a);
+      else go(ps, k_dgrad<8, 8, 2, false, 2>, grid, dim3(512), st, a);
     }
     LAUNCH_CHECK("k_dgrad");
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
@@ -1347,8 +1358,8 @@ static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, floa
   a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
   a.wblocks = m->at.tile_begin[m->at.nw];
   {
-    ProfScope ps(m, "adam_pack", st);
-    k_adam_pack<<<m->adam_blocks, 256, 0, st>>>(a, m->at);
+    ProfScope ps(m, "adam_pack");
+    go(ps, k_adam_pack, dim3(m->adam_blocks), dim3(256), st, a, m->at);
   }
   LAUNCH_CHECK("k_adam_pack");
   k_step_advance<<<1, 1, 0, st>>>(m->dstate, a.b1, a.b2);
