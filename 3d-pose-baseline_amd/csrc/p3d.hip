@@ -16,6 +16,7 @@
 #include <hip/hip_ext.h>
 #include "p3d_kernels.h"
 #include "p3d_bf16.h"
+#include "p3d_eval.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -556,42 +557,6 @@ __global__ __launch_bounds__(256) void k_mse(const float* __restrict__ y, const 
     __syncthreads();
   }
   if (threadIdx.x == 0 && loss) *loss = part[0] / (float)n;
-}
-
-// =====================================================================================
-// MPJPE: un-normalize (fp64) + per-joint L2 of 17 joints, accumulated into joint_sum[17]
-// Bit-for-bit the per-frame arithmetic of predict_3dpose.py:399-430 (no FMA contraction).
-// =====================================================================================
-__global__ __launch_bounds__(256) void k_mpjpe(const float* __restrict__ pred, const float* __restrict__ gt,
-                                               const double* __restrict__ mean, const double* __restrict__ stdv,
-                                               const int32_t* __restrict__ dims, int64_t B, double* joint_sum) {
-  __shared__ double part[16][257];
-  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int j = 0; j < 16; ++j) {
-    double dist = 0.0;
-    if (f < B) {
-      double sq[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const int c = 3 * j + d;
-        const int idx = dims[c];
-        const double pv = __dadd_rn(__dmul_rn((double)pred[f * 48 + c], stdv[idx]), mean[idx]);
-        const double gv = __dadd_rn(__dmul_rn((double)gt[f * 48 + c], stdv[idx]), mean[idx]);
-        const double df = __dsub_rn(pv, gv);
-        sq[d] = __dmul_rn(df, df);
-      }
-      dist = sqrt(__dadd_rn(__dadd_rn(sq[0], sq[1]), sq[2]));
-    }
-    part[j][threadIdx.x] = dist;
-  }
-  __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h)
-      for (int j = 0; j < 16; ++j) part[j][threadIdx.x] += part[j][threadIdx.x + h];
-    __syncthreads();
-  }
-  // joint 0 (root) is mean-vs-mean: distance exactly 0, nothing to add
-  if (threadIdx.x < 16) atomicAdd(joint_sum + 1 + threadIdx.x, part[threadIdx.x][0]);
 }
 
 // =====================================================================================
@@ -1405,16 +1370,29 @@ extern "C" int p3d_set_step(p3d_model* m, int64_t gs, float b1p, float b2p) {
   return P3D_OK;
 }
 
+extern "C" int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const double* mean96,
+                                  const double* std96, const int32_t* dims, int64_t B, int32_t n_joints,
+                                  int32_t procrustes, double* joint_sum, void* stream) {
+  if (!pred_n || !gt_n || !mean96 || !std96 || !dims || !joint_sum)
+    return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: null argument");
+  if (B <= 0) return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: batch must be positive");
+  if (n_joints < 1 || n_joints > P3D_MAX_JOINTS || D <= 0 || D % 3 != 0 ||
+      (3 * n_joints - D != 0 && 3 * n_joints - D != 3))
+    return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: need D == 3*n_joints (predict_14) or 3*(n_joints-1) (root prepended)");
+  MpjpeArgs a{};
+  a.pred = pred_n; a.gt = gt_n; a.D = D; a.J = n_joints; a.root = (3 * n_joints - D) / 3;
+  a.mean = mean96; a.stdv = std96; a.dims = dims; a.B = B; a.joint_sum = joint_sum;
+  const unsigned grid = (unsigned)((B + 255) / 256);
+  if (procrustes) k_mpjpe<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else k_mpjpe<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  LAUNCH_CHECK("k_mpjpe");
+  return P3D_OK;
+}
+
 extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96,
                                const double* std96, const int32_t* dims48, int64_t B, double* joint_sum17,
                                void* stream) {
-  if (!pred_n || !gt_n || !mean96 || !std96 || !dims48 || !joint_sum17)
-    return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: null argument");
-  if (B <= 0) return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: batch must be positive");
-  k_mpjpe<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred_n, gt_n, mean96, std96, dims48, B,
-                                                                         joint_sum17);
-  LAUNCH_CHECK("k_mpjpe");
-  return P3D_OK;
+  return p3d_mpjpe_accum_ex(pred_n, gt_n, 48, mean96, std96, dims48, B, 17, 0, joint_sum17, stream);
 }
 
 extern "C" int p3d_profile_start(p3d_model* m, int32_t max_launches) {

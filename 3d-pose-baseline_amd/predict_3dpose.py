@@ -130,31 +130,38 @@ def get_action_subset(poses_set, action):
 
 
 class MPJPE:
-    """Device accumulator of per-joint L2 sums (p3d_mpjpe_accum), fp64."""
+    """Device accumulator of per-joint L2 sums (p3d_mpjpe_accum_ex), fp64.
+
+    17-joint protocol (root prepended, 48 used dims) or --predict_14 (14 joints, 42 dims);
+    --procrustes aligns every predicted frame to its target first (Protocol #2,
+    src/predict_3dpose.py:413-421)."""
 
     def __init__(self, model, data_mean_3d, data_std_3d, dim_to_use_3d, predict_14=False, procrustes=False):
         import torch
-        if predict_14:
-            raise NotImplementedError("fused MPJPE implements the 17-joint protocol (predict_14 is not fused)")
-        if procrustes:
-            raise NotImplementedError("--procrustes (Protocol #2) is not fused in this build")
         self.torch = torch
         self.model = model
+        self.J = 14 if predict_14 else 17
+        self.D = 3 * self.J if predict_14 else 3 * (self.J - 1)
+        self.procrustes = bool(procrustes)
         dev = model.device
         self.mean = torch.as_tensor(np.asarray(data_mean_3d, np.float64), device=dev)
         self.std = torch.as_tensor(np.asarray(data_std_3d, np.float64), device=dev)
         self.dims = torch.as_tensor(np.asarray(dim_to_use_3d, np.int32), device=dev)
-        if self.mean.numel() != 96 or self.std.numel() != 96 or self.dims.numel() != 48:
-            raise ValueError("MPJPE expects 96-d mean/std and 48 used dims")
-        self.joint_sum = torch.zeros(17, dtype=torch.float64, device=dev)
+        if self.mean.numel() != 96 or self.std.numel() != 96 or self.dims.numel() != self.D:
+            raise ValueError("MPJPE expects 96-d mean/std and %d used dims" % self.D)
+        if model.output_size != self.D:
+            raise ValueError("model predicts %d dims, the %d-joint protocol needs %d"
+                             % (model.output_size, self.J, self.D))
+        self.joint_sum = torch.zeros(self.J, dtype=torch.float64, device=dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
         self.frames = 0
         self.batches = 0
 
     def add(self, pred, gt, loss=None, nbatches=1):
         B = pred.shape[0]
-        check(lib().p3d_mpjpe_accum(ptr(pred), ptr(gt), ptr(self.mean), ptr(self.std), ptr(self.dims), B,
-                                    ptr(self.joint_sum), self.model.stream()), "p3d_mpjpe_accum")
+        check(lib().p3d_mpjpe_accum_ex(ptr(pred), ptr(gt), self.D, ptr(self.mean), ptr(self.std), ptr(self.dims),
+                                       B, self.J, int(self.procrustes), ptr(self.joint_sum), self.model.stream()),
+              "p3d_mpjpe_accum_ex")
         if loss is not None:
             self.loss_sum += loss.double() * nbatches
         self.frames += B
@@ -205,7 +212,7 @@ def evaluate_batches(sess, model, data_mean_3d, data_std_3d, dim_to_use_3d, dim_
     step_time = (time.time() - start) / max(nbatches, 1)
     n = max(acc.frames, 1)
     joint_err = js / n
-    total_err = float(np.sum(js) / (n * 17))
+    total_err = float(np.sum(js) / (n * acc.J))
     return total_err, joint_err, step_time, loss / max(nbatches, 1)
 
 
@@ -216,13 +223,14 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
     Each action's batch list (after the reference's per-action n % B tail drop) is
     split contiguously across the ranks of the current torch.distributed job; every
     rank accumulates fp64 per-joint sums, frame counts and loss sums on its GPU and
-    one all-reduce over a [n_actions, 19] fp64 tensor combines them.  Returns
+    one all-reduce over a [n_actions, J+2] fp64 tensor combines them.  Returns
     ({action: mm}, average_mm) with the reference's unweighted Average.
     """
     import torch
     flags = flags or FLAGS
     _, rank, world = dist_utils.dist_state()
-    table = torch.zeros((len(actions), 19), dtype=torch.float64, device=model.device)
+    J = 14 if flags.predict_14 else 17
+    table = torch.zeros((len(actions), J + 2), dtype=torch.float64, device=model.device)
     with torch.cuda.device(model.device):
         for ai, action in enumerate(actions):
             enc, dec = model.get_all_batches(get_action_subset(test_set_2d, action),
@@ -234,15 +242,15 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
                 X = torch.from_numpy(_stack(enc[lo:hi], model.input_size)).to(model.device)
                 Y = torch.from_numpy(_stack(dec[lo:hi], model.output_size)).to(model.device)
                 run_eval_rows(model, acc, X, Y, model.batch_size)
-            table[ai, :17] = acc.joint_sum
-            table[ai, 17] = float(acc.frames)
-            table[ai, 18] = acc.loss_sum[0]
+            table[ai, :J] = acc.joint_sum
+            table[ai, J] = float(acc.frames)
+            table[ai, J + 1] = acc.loss_sum[0]
         dist_utils.allreduce_sum_(table)
         t = table.cpu().numpy()
     errs = {}
     for ai, action in enumerate(actions):
-        n = max(t[ai, 17], 1.0)
-        errs[action] = float(np.sum(t[ai, :17]) / (n * 17))
+        n = max(t[ai, J], 1.0)
+        errs[action] = float(np.sum(t[ai, :J]) / (n * J))
     return errs, float(np.mean([errs[a] for a in actions]))
 
 
@@ -250,7 +258,7 @@ def synthetic_h36m(n_train=20000, n_test=4000, seed=0, out_dim=48):
     """Normalized H3.6M-shaped data (keys (subject, action, seqname)) and stats."""
     rng = np.random.default_rng(seed)
     actions = data_utils.define_actions("All")
-    use3, ign3 = data_utils.dimension_sets(3)
+    use3, ign3 = data_utils.dimension_sets(3, out_dim == 42)
     use2, ign2 = data_utils.dimension_sets(2)
     mean3 = np.zeros(96)
     std3 = np.zeros(96)

@@ -133,10 +133,20 @@ int p3d_set_step(p3d_model* m, int64_t global_step, float beta1_power, float bet
  *   mean96/std96 [96] fp64 (data_mean_3d / data_std_3d), dims48 [48] int32
  *   (dim_to_use_3d).  Un-normalizes both (x*std+mean, fp64, root dims = mean),
  *   takes the 17 joints [0,1,2] + dims48, and ADDS per-joint L2 sums (fp64) into
- *   joint_sum17[17].  Procrustes is not fused here. */
+ *   joint_sum17[17]. */
 int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96,
                     const double* std96, const int32_t* dims48, int64_t B, double* joint_sum17,
                     void* stream);
+
+/* General form (src/predict_3dpose.py:383,399-430 with FLAGS.predict_14 / FLAGS.procrustes):
+ *   D = 48, n_joints = 17: the 17-joint protocol above (root joint prepended);
+ *   D = 42, n_joints = 14: --predict_14 (dims = the 42 dim_to_use_3d, no root);
+ *   procrustes != 0: per-frame similarity alignment of the prediction onto the target
+ *   (src/procrustes.py:2-63, compute_optimal_scale=True) before the per-joint L2.
+ * ADDS into joint_sum[n_joints]. */
+int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const double* mean96,
+                       const double* std96, const int32_t* dims, int64_t B, int32_t n_joints,
+                       int32_t procrustes, double* joint_sum, void* stream);
 
 /* Live kernel timing (bench.py's roofline): while active, every kernel the model
  * launches is bracketed by a hipEvent pair.  p3d_profile_stop synchronises and writes

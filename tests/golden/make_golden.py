@@ -98,6 +98,43 @@ for scale in (True, False):
                 "pr_%s_b" % tag: np.array(b), "pr_%s_c" % tag: c})
 out.update(pr_X=X, pr_Y=Y)
 
+# --- predict_14 protocol (14 joints, no root prefix) + procrustes, and reflected poses ---
+def mpjpe_dists(pred_n_, gt_n_, mean_, std_, ign_, use_, n_joints, proc):
+    dec_ = data_utils.unNormalizeData(gt_n_, mean_, std_, ign_)
+    pose_ = data_utils.unNormalizeData(pred_n_, mean_, std_, ign_)
+    dtu = np.hstack((np.arange(3), use_)) if n_joints == 17 else use_
+    dec_, pose_ = dec_[:, dtu], pose_[:, dtu]
+    if proc:
+        for j in range(pose_.shape[0]):
+            g_ = np.reshape(dec_[j, :], [-1, 3])
+            o_ = np.reshape(pose_[j, :], [-1, 3])
+            _, Z_, T_, b_, c_ = procrustes.compute_similarity_transform(g_, o_, compute_optimal_scale=True)
+            pose_[j, :] = np.reshape((b_ * o_.dot(T_)) + c_, [-1, n_joints * 3])
+    sq_ = (pose_ - dec_) ** 2
+    dd = np.zeros((pose_.shape[0], n_joints))
+    for j, k in enumerate(np.arange(0, n_joints * 3, 3)):
+        dd[:, j] = np.sqrt(np.sum(sq_[:, k:k + 3], axis=1))
+    return dd
+
+
+mean14 = np.zeros(96)
+std14 = np.zeros(96)
+mean14[use3_14] = rng.uniform(-500, 500, len(use3_14))
+std14[use3_14] = rng.uniform(50, 300, len(use3_14))
+pred14 = rng.standard_normal((64, 42)).astype(np.float32)
+gt14 = rng.standard_normal((64, 42))
+out.update(mp14_mean=mean14, mp14_std=std14, mp14_pred_n=pred14, mp14_gt_n=gt14,
+           mp14_dists=mpjpe_dists(pred14, gt14, mean14, std14, ign3_14, use3_14, 14, False),
+           mp14_dists_procrustes=mpjpe_dists(pred14, gt14, mean14, std14, ign3_14, use3_14, 14, True))
+# mirrored predictions (det < 0 branch of compute_similarity_transform) + small noise
+gtr = rng.standard_normal((32, 48))
+decr = data_utils.unNormalizeData(gtr, mean3, std3, ign3)
+mir = decr.copy()
+mir[:, 0::3] = -mir[:, 0::3]
+predr = ((mir[:, use3] - mean3[use3]) / std3[use3] + rng.normal(0, 0.01, (32, 48))).astype(np.float32)
+out.update(mpr_pred_n=predr, mpr_gt_n=gtr,
+           mpr_dists_procrustes=mpjpe_dists(predr, gtr, mean3, std3, ign3, use3, 17, True))
+
 # --- define_actions -----------------------------------------------------------------
 out["actions"] = np.array(data_utils.define_actions("All"))
 

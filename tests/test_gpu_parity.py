@@ -143,6 +143,51 @@ def test_mpjpe_kernel_matches_reference_goldens():
     m.close()
 
 
+@pytest.mark.parametrize("case", ["17", "17_procrustes", "14", "14_procrustes", "mirror_procrustes"])
+def test_mpjpe_protocols_match_reference_goldens(case):
+    """p3d_mpjpe_accum_ex vs the reference's own evaluate_batches arithmetic
+    (tests/golden/make_golden.py): bit-exact sums without Procrustes up to the order of
+    the fp64 atomics (1e-12 rel); Procrustes (Jacobi eigensolver vs LAPACK SVD) to 1e-9 mm
+    per joint-sum."""
+    g = np.load("tests/golden/reference_goldens.npz", allow_pickle=False)
+    p14 = case.startswith("14")
+    proc = case.endswith("procrustes")
+    if p14:
+        pred, gt, mean, std, use = g["mp14_pred_n"], g["mp14_gt_n"], g["mp14_mean"], g["mp14_std"], g["ns_use3_14"]
+        ref = g["mp14_dists_procrustes" if proc else "mp14_dists"]
+    elif case.startswith("mirror"):
+        pred, gt, mean, std, use = g["mpr_pred_n"], g["mpr_gt_n"], g["nd_mean"], g["nd_std"], g["ns_use3"]
+        ref = g["mpr_dists_procrustes"]
+    else:
+        pred, gt, mean, std, use = g["mp_pred_n"], g["mp_gt_n"], g["nd_mean"], g["nd_std"], g["ns_use3"]
+        ref = g["mp_dists_procrustes" if proc else "mp_dists"]
+    L = 256
+    m = linear_model.LinearModel(L, 1, True, True, False, 64, 1e-3, "/tmp/p3d_test", p14, seed=1)
+    acc = predict_3dpose.MPJPE(m, mean, std, use, predict_14=p14, procrustes=proc)
+    acc.add(torch.from_numpy(np.ascontiguousarray(pred)).cuda(),
+            torch.from_numpy(np.ascontiguousarray(gt, dtype=np.float32)).cuda())
+    js = acc.joint_sum.cpu().numpy()
+    assert js.shape == (14 if p14 else 17,)
+    tol = dict(rtol=1e-9, atol=1e-9) if proc else dict(rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(js, ref.sum(axis=0), **tol)
+    m.close()
+
+
+def test_mpjpe_procrustes_large_batch_vs_oracle():
+    """Ragged multi-block batch (B = 1000): Procrustes MPJPE vs the numpy oracle."""
+    stats = ref_eval.synthetic_stats()
+    rng = np.random.default_rng(7)
+    pred = rng.standard_normal((1000, 48)).astype(np.float32)
+    gt = rng.standard_normal((1000, 48)).astype(np.float32)
+    ref = ref_eval.batch_dists(pred, gt.astype(np.float64), stats["mean3"], stats["std3"], stats["ign3"],
+                               stats["use3"], procrustes=True)
+    m = linear_model.LinearModel(256, 1, True, True, False, 64, 1e-3, "/tmp/p3d_test", seed=1)
+    acc = predict_3dpose.MPJPE(m, stats["mean3"], stats["std3"], stats["use3"], procrustes=True)
+    acc.add(torch.from_numpy(pred).cuda(), torch.from_numpy(gt).cuda())
+    np.testing.assert_allclose(acc.joint_sum.cpu().numpy(), ref.sum(axis=0), rtol=1e-9, atol=1e-8)
+    m.close()
+
+
 def test_mpjpe_end_to_end_within_1e4_mm():
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     st, m = make(cfg)

@@ -63,6 +63,18 @@ def test_mpjpe_dists_match_reference(g):
     np.testing.assert_allclose(dp, g["mp_dists_procrustes"], rtol=1e-12, atol=1e-10)
 
 
+def test_mpjpe_predict14_and_mirrored_match_reference(g):
+    ign14 = g["ns_ign3_14"]
+    for proc, key in ((False, "mp14_dists"), (True, "mp14_dists_procrustes")):
+        d = ref_eval.batch_dists(g["mp14_pred_n"], g["mp14_gt_n"], g["mp14_mean"], g["mp14_std"], ign14,
+                                 g["ns_use3_14"], predict_14=True, procrustes=proc)
+        np.testing.assert_allclose(d, g[key], rtol=1e-12, atol=1e-10)
+    # mirrored predictions: the det < 0 branch of compute_similarity_transform
+    d = ref_eval.batch_dists(g["mpr_pred_n"], g["mpr_gt_n"], g["nd_mean"], g["nd_std"], g["ns_ign3"],
+                             g["ns_use3"], procrustes=True)
+    np.testing.assert_allclose(d, g["mpr_dists_procrustes"], rtol=1e-12, atol=1e-10)
+
+
 def test_procrustes_matches_reference(g):
     for tag, scale in (("s", True), ("n", False)):
         d, Z, T, b, c = ref_eval.compute_similarity_transform(g["pr_X"], g["pr_Y"], compute_optimal_scale=scale)
