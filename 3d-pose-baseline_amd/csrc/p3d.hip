@@ -17,6 +17,7 @@
 #include "p3d_kernels.h"
 #include "p3d_bf16.h"
 #include "p3d_eval.h"
+#include "p3d_gemm.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -698,6 +699,8 @@ struct p3d_model {
   // workgroups co-reside per CU, so independent batches on different streams overlap
   // (tools/streams_sweep2.py: 4 streams 5.6 M poses/s vs 4.9 M with 16-wave workgroups).
   int infer_wk = 8;
+  int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
+  int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -902,6 +905,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev) == 8 ? 8 : 16;
+  if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
+  if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   {
     StepState s0{};
     s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
@@ -1044,7 +1049,42 @@ static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch
   }
 }
 
+// Large-M inference hidden layer (p3d_gemm.h): 128x128 tiles, grid = ceil(M/128) * N/128.
+static bool use_big(const p3d_model* m, const FwdArgs& a, int kind, bool whole_batch) {
+  return kind == 1 && !whole_batch && m->big_m > 0 && a.M >= m->big_m && a.N % 128 == 0 &&
+         a.K % 32 == 0 &&
+         a.bn != 2 && !a.z_save && a.ldy == 0;
+}
+
+static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
+  GemmF32Args g{};
+  g.A = a.X; g.Wf = a.Wf; g.bias = a.bias; g.wsq = a.wsq;
+  g.M = a.M; g.K = a.K; g.N = a.N;
+  g.bn = a.bn; g.gamma = a.gamma; g.beta = a.beta; g.mmean = a.mmean; g.mvar = a.mvar; g.eps = a.eps;
+  g.relu = a.relu; g.keep = a.keep; g.seed = a.seed; g.ctr = a.ctr; g.site = a.site; g.row_off = a.row_off;
+  g.ctr_dev = a.ctr_dev; g.res = a.res; g.Y = a.Y;
+  const unsigned grid = (unsigned)(((a.M + 127) / 128) * (a.N / 128));
+  ProfScope ps(m, "fwd_hidden_big");
+  // big_depth selects the LDS ring: 1 -> 1 k-group x 4 stages (64 KB, two workgroups per
+  // CU), 2 -> 2 k-groups x 3 stages (96 KB), 3 -> 2 k-groups x 2 stages (64 KB)
+  if (m->big_depth == 2) go(ps, k_gemm_f32<2, 3>, dim3(grid), dim3(256), st, g);
+  else if (m->big_depth == 3) go(ps, k_gemm_f32<2, 2>, dim3(grid), dim3(256), st, g);
+  else go(ps, k_gemm_f32<1, 4>, dim3(grid), dim3(256), st, g);
+}
+
 static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch, hipStream_t st) {
+  if (use_big(m, a, kind, whole_batch)) {
+    launch_big(m, a, st);
+    LAUNCH_CHECK("k_gemm_f32");
+    return P3D_OK;
+  }
+  if (kind == 0 && !whole_batch && m->big_m > 0 && a.M >= m->big_m) {
+    // input layer (K = 32: two k-groups) at large M: 64 rows x 16 columns per wave
+    ProfScope ps(m, "fwd_in_big");
+    go(ps, k_fwd<4, 2, 2, 2, false, true, 0>, dim3((a.N + 15) / 16, (a.M + 63) / 64), dim3(128), st, a);
+    LAUNCH_CHECK("k_fwd");
+    return P3D_OK;
+  }
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind]);
@@ -1372,7 +1412,7 @@ extern "C" int p3d_set_step(p3d_model* m, int64_t gs, float b1p, float b2p) {
 
 extern "C" int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const double* mean96,
                                   const double* std96, const int32_t* dims, int64_t B, int32_t n_joints,
-                                  int32_t procrustes, double* joint_sum, void* stream) {
+                                  int32_t procrustes, double* joint_sum, double* sq_sum, void* stream) {
   if (!pred_n || !gt_n || !mean96 || !std96 || !dims || !joint_sum)
     return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: null argument");
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: batch must be positive");
@@ -1381,10 +1421,10 @@ extern "C" int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_
     return fail(P3D_ERR_ARG, "p3d_mpjpe_accum: need D == 3*n_joints (predict_14) or 3*(n_joints-1) (root prepended)");
   MpjpeArgs a{};
   a.pred = pred_n; a.gt = gt_n; a.D = D; a.J = n_joints; a.root = (3 * n_joints - D) / 3;
-  a.mean = mean96; a.stdv = std96; a.dims = dims; a.B = B; a.joint_sum = joint_sum;
-  const unsigned grid = (unsigned)((B + 255) / 256);
-  if (procrustes) k_mpjpe<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-  else k_mpjpe<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  a.mean = mean96; a.stdv = std96; a.dims = dims; a.B = B; a.joint_sum = joint_sum; a.sq_sum = sq_sum;
+  const unsigned grid = (unsigned)((B + 63) / 64);
+  if (procrustes) k_mpjpe<true><<<grid, 64, 0, (hipStream_t)stream>>>(a);
+  else k_mpjpe<false><<<grid, 64, 0, (hipStream_t)stream>>>(a);
   LAUNCH_CHECK("k_mpjpe");
   return P3D_OK;
 }
@@ -1392,7 +1432,7 @@ extern "C" int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_
 extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96,
                                const double* std96, const int32_t* dims48, int64_t B, double* joint_sum17,
                                void* stream) {
-  return p3d_mpjpe_accum_ex(pred_n, gt_n, 48, mean96, std96, dims48, B, 17, 0, joint_sum17, stream);
+  return p3d_mpjpe_accum_ex(pred_n, gt_n, 48, mean96, std96, dims48, B, 17, 0, joint_sum17, nullptr, stream);
 }
 
 extern "C" int p3d_profile_start(p3d_model* m, int32_t max_launches) {

@@ -22,6 +22,7 @@ struct MpjpeArgs {
   const double* mean; const double* stdv; const int32_t* dims;   // [96], [96], [D]
   int64_t B;
   double* joint_sum;                    // [J] (+=)
+  double* sq_sum;                       // [1] (+=) sum of (pred_n - gt_n)^2, or null
 };
 
 // joint j of one frame, un-normalized (mm)
@@ -128,13 +129,23 @@ __device__ void p3d_procrustes_rot(const double A[3][3], double T[3][3], double*
   *traceTA = s1 + s2 + g * fabs(sig3);
 }
 
+// 64 frames per workgroup (one wave): many small workgroups spread the per-frame
+// dependent loads over the whole chip.
 template <bool PROC>
-__global__ __launch_bounds__(256) void k_mpjpe(MpjpeArgs a) {
-  __shared__ double part[P3D_MAX_JOINTS][257];
-  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void k_mpjpe(MpjpeArgs a) {
+  __shared__ double part[P3D_MAX_JOINTS][65];
+  const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const bool live = f < a.B;
   const float* prow = a.pred + (live ? f : 0) * a.D;
   const float* grow = a.gt + (live ? f : 0) * a.D;
+  double sq_frame = 0.0;
+  if (a.sq_sum && live) {
+    // the loss of src/linear_model.py:129 in normalized space (fp32 differences/squares)
+    for (int c = 0; c < a.D; ++c) {
+      const float d = prow[c] - grow[c];
+      sq_frame += (double)(d * d);
+    }
+  }
   if (!PROC) {
     for (int j = 0; j < a.J; ++j) {
       double dist = 0.0;
@@ -201,13 +212,13 @@ __global__ __launch_bounds__(256) void k_mpjpe(MpjpeArgs a) {
     }
   }
   __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h)
-      for (int j = 0; j < a.J; ++j) part[j][threadIdx.x] += part[j][threadIdx.x + h];
-    __syncthreads();
-  }
   if ((int)threadIdx.x < a.J) {
-    const double s = part[threadIdx.x][0];
+    double s = 0.0;
+    for (int t = 0; t < 64; ++t) s += part[threadIdx.x][t];
     if (s != 0.0) atomicAdd(a.joint_sum + threadIdx.x, s);
+  }
+  if (a.sq_sum) {
+    for (int o = 32; o > 0; o >>= 1) sq_frame += __shfl_xor(sq_frame, o, 64);
+    if (threadIdx.x == 0) atomicAdd(a.sq_sum, sq_frame);
   }
 }

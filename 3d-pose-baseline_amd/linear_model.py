@@ -361,11 +361,12 @@ class LinearModel(object):
             t = t.to(device=self.device, dtype=torch.float32, non_blocking=True).contiguous()
         return t
 
-    def forward_device(self, x, training=False, keep_prob=1.0, out=None, ctr=None, ws_row=0):
+    def forward_device(self, x, training=False, keep_prob=1.0, out=None, ctr=None, ws_row=0, row_offset=None):
         """Device-resident forward: returns outputs [B, output_size] (no host sync).
 
         ``ws_row`` (inference only) selects the workspace rows this call uses, so that
-        independent batches on different streams can run concurrently."""
+        independent batches on different streams can run concurrently.  ``row_offset``
+        is the global row index of x[0] in the dropout counter (default rank * B)."""
         x = self._as_dev(x, self.input_size, "enc_in")
         B = x.shape[0]
         if out is None:
@@ -373,7 +374,8 @@ class LinearModel(object):
         if ctr is None:
             ctr = _p3d.P3D_CTR_GLOBAL_STEP if training else 0
         check(lib().p3d_forward_ex(self._h, ptr(x), B, ptr(out), int(bool(training)), float(keep_prob),
-                                   self.seed, int(ctr), self.rank * B, int(ws_row), self.stream()), "p3d_forward")
+                                   self.seed, int(ctr), self.rank * B if row_offset is None else int(row_offset),
+                                   int(ws_row), self.stream()), "p3d_forward")
         return out
 
     def loss_device(self, y, t, dy=None):

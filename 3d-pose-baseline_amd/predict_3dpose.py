@@ -112,7 +112,7 @@ def create_model(session, actions, batch_size, flags=None):
     model = linear_model.LinearModel(flags.linear_size, flags.num_layers, flags.residual, flags.batch_norm,
                                      flags.max_norm, batch_size, flags.learning_rate,
                                      os.path.join(tdir, "log"), flags.predict_14, seed=flags.seed,
-                                     max_batch=max(batch_size, 4096))
+                                     max_batch=max(batch_size, 8192))
     if flags.load <= 0:
         print("Creating model with fresh parameters.")
         return model
@@ -152,20 +152,31 @@ class MPJPE:
         if model.output_size != self.D:
             raise ValueError("model predicts %d dims, the %d-joint protocol needs %d"
                              % (model.output_size, self.J, self.D))
-        self.joint_sum = torch.zeros(self.J, dtype=torch.float64, device=dev)
-        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        # [0:J] per-joint L2 sums (mm), [J] sum of squared normalized errors (the loss
+        # numerator of src/linear_model.py:129), both fp64, accumulated by the kernel
+        self.sums = torch.zeros(self.J + 1, dtype=torch.float64, device=dev)
+        self.joint_sum = self.sums[:self.J]
+        self.sq_sum = self.sums[self.J:]
         self.frames = 0
         self.batches = 0
 
-    def add(self, pred, gt, loss=None, nbatches=1):
+    def reset(self):
+        self.sums.zero_()
+        self.frames = 0
+        self.batches = 0
+
+    def add(self, pred, gt, nbatches=None):
+        """Accumulate one device batch of B frames (B = nbatches * batch_size rows)."""
         B = pred.shape[0]
         check(lib().p3d_mpjpe_accum_ex(ptr(pred), ptr(gt), self.D, ptr(self.mean), ptr(self.std), ptr(self.dims),
-                                       B, self.J, int(self.procrustes), ptr(self.joint_sum), self.model.stream()),
-              "p3d_mpjpe_accum_ex")
-        if loss is not None:
-            self.loss_sum += loss.double() * nbatches
+                                       B, self.J, int(self.procrustes), ptr(self.joint_sum), ptr(self.sq_sum),
+                                       self.model.stream()), "p3d_mpjpe_accum_ex")
         self.frames += B
-        self.batches += nbatches
+        self.batches += 1 if nbatches is None else nbatches
+
+    def loss_sum(self, batch_size):
+        """Device scalar: sum over batches of the per-batch loss mean((y - t)^2)."""
+        return self.sq_sum / float(batch_size * self.D)
 
 
 def _stack(batches, width):
@@ -174,7 +185,7 @@ def _stack(batches, width):
     return np.ascontiguousarray(np.vstack(batches), dtype=np.float32)
 
 
-def run_eval_rows(model, acc, X, Y, batch_size, chunk_rows=4096):
+def run_eval_rows(model, acc, X, Y, batch_size, chunk_rows=8192):
     """Forward + fused MPJPE over whole batches of device rows X/Y (no host sync).
 
     Inference rows are independent (BN uses moving statistics), so consecutive
@@ -187,8 +198,7 @@ def run_eval_rows(model, acc, X, Y, batch_size, chunk_rows=4096):
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         y = model.forward_device(X[s:e], False, 1.0, out=out[:e - s])
-        loss = model.loss_device(y, Y[s:e])
-        acc.add(y, Y[s:e], loss, (e - s) // batch_size)
+        acc.add(y, Y[s:e], (e - s) // batch_size)
 
 
 def evaluate_batches(sess, model, data_mean_3d, data_std_3d, dim_to_use_3d, dim_to_ignore_3d,
@@ -208,7 +218,7 @@ def evaluate_batches(sess, model, data_mean_3d, data_std_3d, dim_to_use_3d, dim_
         Y = torch.from_numpy(_stack(decoder_outputs, model.output_size)).to(model.device)
         run_eval_rows(model, acc, X, Y, model.batch_size)
         js = acc.joint_sum.cpu().numpy()
-        loss = float(acc.loss_sum.item())
+        loss = float(acc.loss_sum(model.batch_size).item())
     step_time = (time.time() - start) / max(nbatches, 1)
     n = max(acc.frames, 1)
     joint_err = js / n
@@ -244,7 +254,7 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
                 run_eval_rows(model, acc, X, Y, model.batch_size)
             table[ai, :J] = acc.joint_sum
             table[ai, J] = float(acc.frames)
-            table[ai, J + 1] = acc.loss_sum[0]
+            table[ai, J + 1] = acc.loss_sum(model.batch_size)[0]
         dist_utils.allreduce_sum_(table)
         t = table.cpu().numpy()
     errs = {}

@@ -5,13 +5,16 @@
 Modes (BASELINE.json configs):
   infer  (default, configs[1]) L=1024, 2 residual blocks, BN, batch 64, fp32 inference.
          One step = one forward pass over one batch of 64 poses (its own synthetic
-         batch, resident in HBM).  Steps are issued back to back on one stream and
-         replayed from a HIP graph of G steps (launch overhead amortised; every step
-         still runs its own six layer kernels over its own 64 rows).
+         batch, resident in HBM).  S = 4 streams (one per hardware queue) each replay
+         their own HIP graph of steps over a private workspace slot, so independent
+         batches overlap; every step still runs its own six layer kernels over its own
+         64 rows.  The single-stream rate is reported as "single_stream".
   train  (configs[2]) same model, one step = fwd + MSE + bwd + [RCCL all-reduce] +
          TF1 Adam at batch 64 per GPU, keep_prob 0.5.
   eval   (configs[3]) evaluateActionWise sweep over a synthetic 15-action H3.6M-shaped
-         test set, batches sharded across ranks, one all-reduce of per-action sums.
+         test set, batches sharded across ranks, one all-reduce of per-action sums
+         (also reported as "eval_sweep" beside the default infer line).
+  stress (configs[4]) L=4096, 4 blocks, bf16/fp32-acc, batch 1024 inference.
 
 Multi-GPU: one process per GPU (torch.distributed.run); inference shards by batch
 with no data-path collective (scaling "weak"); train is data parallel (RCCL).
@@ -309,6 +312,82 @@ def bench_train(args, rank, world, steps=None, warmup=None):
     return value, dt, roof, ("graph" if use_graph else "eager")
 
 
+def bench_eval(args, rank, world):
+    """cfg4: evaluateActionWise sweep (src/predict_3dpose.py:274-298) over a synthetic
+    H3.6M-shaped test set: 15 actions, N_a ~ U[20000, 40000] frames (seed 4), the
+    reference's per-action n % 64 tail drop, each action's batches split contiguously
+    across ranks.  One sweep = forward (BN eval, keep 1) + MSE loss + fused MPJPE of
+    every batch, then one all-reduce of the [15, 19] fp64 per-action table and its copy
+    to the host (the per-action numbers the reference prints).  Inputs are resident in
+    HBM; independent batches are submitted --eval-chunk rows per launch."""
+    import torch
+    import data_utils
+    import dist_utils
+    import predict_3dpose
+    chunk = args.eval_chunk
+    model, _ = make_model(data_parallel=False, max_batch=chunk)
+    rng = np.random.default_rng(4)
+    nb = [int(n) // BATCH for n in rng.integers(20000, 40001, 15)]
+    shares = [dist_utils.shard_range(b, rank, world) for b in nb]
+    rows = [(hi - lo) * BATCH for lo, hi in shares]
+    g = np.random.default_rng(40 + rank)
+    X = torch.from_numpy(g.standard_normal((sum(rows), IN)).astype(np.float32)).cuda()
+    Y = torch.from_numpy(g.standard_normal((sum(rows), OUT)).astype(np.float32)).cuda()
+    use3, _ = data_utils.dimension_sets(3)
+    sr = np.random.default_rng(3)
+    mean3, std3 = np.zeros(96), np.zeros(96)
+    mean3[use3] = sr.uniform(-500, 500, len(use3))
+    std3[use3] = sr.uniform(50, 300, len(use3))
+    accs = [predict_3dpose.MPJPE(model, mean3, std3, use3, procrustes=args.procrustes) for _ in nb]
+    table = torch.zeros((len(nb), 19), dtype=torch.float64, device="cuda")
+
+    def sweep():
+        off = 0
+        for a, acc in enumerate(accs):
+            acc.reset()
+            if rows[a]:
+                predict_3dpose.run_eval_rows(model, acc, X[off:off + rows[a]], Y[off:off + rows[a]], BATCH,
+                                             chunk_rows=chunk)
+            off += rows[a]
+            table[a, :17] = acc.joint_sum
+            table[a, 17] = float(acc.frames)
+            table[a, 18] = acc.loss_sum(BATCH)[0]
+        dist_utils.allreduce_sum_(table)
+        return table.cpu().numpy()
+
+    for _ in range(2):
+        sweep()
+    reps = max(1, args.eval_reps)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        t = sweep()
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world) / reps
+    frames = sum(nb) * BATCH
+    assert int(round(t[:, 17].sum())) == frames, (t[:, 17].sum(), frames)
+    errs = t[:, :17].sum(1) / (t[:, 17] * 17)
+    # dominant kernel of the sweep: a hidden layer at M = chunk rows (k_gemm_f32 when
+    # chunk >= 256), timed live with dispatch-attached events
+    import _p3d
+    lay = lambda n: _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, chunk, n, model.stream()), "p3d_time_layer")
+    lay(5)
+    prof = profile_kernels(model, lambda: lay(50))
+    tag = "fwd_hidden_big" if "fwd_hidden_big" in prof else "fwd_hidden"
+    avg_us = prof[tag][1]
+    flop = 2.0 * chunk * L * L
+    roof = {"bound": "mfma", "achieved": round(flop / (avg_us * 1e-6) / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flop / (avg_us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "kernel": "k_gemm_f32<2> (hidden layer, 128x128 tiles)" if tag == "fwd_hidden_big" else "k_fwd",
+            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3)}
+    model.close()
+    return {"workload": "cfg4 evaluateActionWise sweep: 15 actions, %d frames (tail-dropped), %s, "
+                        "%d-row launches, sharded over %d rank(s)"
+                        % (frames, "Protocol #2 (Procrustes)" if args.procrustes else "Protocol #1", chunk, world),
+            "value": round(frames / dt, 1), "unit": "frames/s", "ms_per_sweep": round(1000.0 * dt, 3),
+            "average_mm": round(float(np.mean(errs)), 6), "roofline": roof}
+
+
 def bench_stress(args, rank, world):
     """cfg5: L=4096, 4 residual blocks, bf16 weights/activations with fp32 accumulate and
     fp32 BN, batch 1024, inference.  One step = one forward of one batch of 1024 poses."""
@@ -370,20 +449,24 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--mode", choices=["infer", "train", "stress"], default="infer")
+    ap.add_argument("--mode", choices=["infer", "train", "eval", "stress"], default="infer")
     ap.add_argument("--graph-steps", type=int, default=240)
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
     ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
+    ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
+    ap.add_argument("--eval-reps", type=int, default=5)
+    ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
+    ap.add_argument("--procrustes", action="store_true", help="cfg4 sweep with Protocol #2 alignment")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
     rank, world, local = setup_dist()
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    train = single = None
+    train = single = sweep = None
     if args.mode == "infer":
         value, dt, roof, single = bench_infer(args, rank, world)
         workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
@@ -397,6 +480,16 @@ def main():
                          "roofline": troof}
             except Exception as exc:  # report, never lose the headline line
                 train = {"error": repr(exc)[:300]}
+        if not args.no_eval:
+            try:
+                sweep = bench_eval(args, rank, world)
+            except Exception as exc:
+                sweep = {"error": repr(exc)[:300]}
+    elif args.mode == "eval":
+        sweep = bench_eval(args, rank, world)
+        value, dt, roof = sweep["value"], sweep["ms_per_sweep"] / 1000.0, sweep.pop("roofline")
+        args.steps = 1
+        workload = sweep["workload"]
     elif args.mode == "stress":
         value, dt, roof, args.steps = bench_stress(args, rank, world)
         workload = "cfg5 inference: L=4096, 4 residual blocks, BN(eval), batch 1024 per step, bf16/fp32-acc"
@@ -408,8 +501,10 @@ def main():
         cpu = None if args.no_cpu else cpu_baseline(args.mode, args.cpu_seconds)
         if args.mode == "stress":
             cpu = None
-        line = {"metric": "poses/sec at batch 64 (H3.6M 16-joint)" if args.mode != "stress" else
-                "poses/sec at batch 1024 (cfg5 bf16 stress)", "value": round(value, 1), "unit": "poses/s",
+        metric = {"stress": "poses/sec at batch 1024 (cfg5 bf16 stress)",
+                  "eval": "frames/sec, evaluateActionWise MPJPE sweep (cfg4)"}.get(
+                      args.mode, "poses/sec at batch 64 (H3.6M 16-joint)")
+        line = {"metric": metric, "value": round(value, 1), "unit": "frames/s" if args.mode == "eval" else "poses/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(1000.0 * dt / args.steps, 5), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.mode == "stress" else "f32",
@@ -423,6 +518,8 @@ def main():
             line["single_stream"] = single
         if train is not None:
             line["train"] = train
+        if sweep is not None and args.mode != "eval":
+            line["eval_sweep"] = sweep
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

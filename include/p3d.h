@@ -143,10 +143,11 @@ int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const double* mean96
  *   D = 42, n_joints = 14: --predict_14 (dims = the 42 dim_to_use_3d, no root);
  *   procrustes != 0: per-frame similarity alignment of the prediction onto the target
  *   (src/procrustes.py:2-63, compute_optimal_scale=True) before the per-joint L2.
- * ADDS into joint_sum[n_joints]. */
+ * ADDS into joint_sum[n_joints]; if sq_sum is non-null also adds sum((pred_n - gt_n)^2)
+ * over the B x D batch (the loss of src/linear_model.py:129 times B*D, fp64 sum). */
 int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const double* mean96,
                        const double* std96, const int32_t* dims, int64_t B, int32_t n_joints,
-                       int32_t procrustes, double* joint_sum, void* stream);
+                       int32_t procrustes, double* joint_sum, double* sq_sum, void* stream);
 
 /* Live kernel timing (bench.py's roofline): while active, every kernel the model
  * launches is bracketed by a hipEvent pair.  p3d_profile_stop synchronises and writes

@@ -67,6 +67,27 @@ def test_eval_variants(residual, batch_norm, max_norm):
     m.close()
 
 
+@pytest.mark.parametrize("B,residual,batch_norm,max_norm,keep", [
+    (256, True, True, False, 1.0), (1000, True, True, False, 1.0), (4096, True, True, False, 1.0),
+    (777, False, True, True, 1.0), (300, True, False, False, 1.0), (1000, True, True, False, 0.5)])
+def test_eval_forward_large_batch(B, residual, batch_norm, max_norm, keep):
+    """Large-M inference path (k_gemm_f32, M >= 256): 128x128 tiles, ragged tails,
+    fused eval-BN / ReLU / dropout / residual epilogue vs the oracle."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=residual, batch_norm=batch_norm,
+                      max_norm=max_norm)
+    st, m = make(cfg, batch=64, max_batch=B)
+    rng = np.random.default_rng(B)
+    x = rng.standard_normal((B, 32)).astype(np.float32)
+    y = m.forward_device(torch.from_numpy(x).cuda(), False, keep, ctr=5).cpu().numpy()
+    ro, _ = ref_mlp.forward(st, x, False, keep, m.seed, 5, 0)
+    close(y, ro, atol=5e-5, rtol=5e-5)
+    # rows are independent: the same frames through the batch-64 kernels agree
+    y64 = np.concatenate([m.forward_device(torch.from_numpy(x[i:i + 64]).cuda(), False, keep, ctr=5,
+                                           row_offset=i).cpu().numpy() for i in range(0, B, 64)])
+    close(y, y64, atol=5e-5, rtol=5e-5)
+    m.close()
+
+
 def _grad_check(cfg, keep, B=64):
     st, m = make(cfg, batch=B)
     rng = np.random.default_rng(9)
