@@ -12,7 +12,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libp3d.so")
+LIB_PATH = os.environ.get("P3D_LIB", os.path.join(HERE, "libp3d.so"))  # P3D_LIB: dev builds (tools/)
 
 P3D_CTR_GLOBAL_STEP = 0xFFFFFFFFFFFFFFFF
 P3D_DTYPE_F32 = 0

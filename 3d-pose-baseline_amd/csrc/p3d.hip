@@ -48,7 +48,23 @@ struct FwdArgs {
   const int64_t* ctr_dev;         // if set, dropout counter = *ctr_dev (device global_step)
   const float* res;               // residual added after dropout, packed [M, N]
   float* Y; int64_t ldy;          // packed (hidden) or row-major (output layer)
+  float* bnpart;                  // bn == 3: per (row tile, column) {sum z, sum (z - tile mean)^2}
 };
+
+// Phase timestamps for kernel development (build with -DP3D_TRACE; tools/trace_train.py).
+#ifdef P3D_TRACE
+__device__ unsigned long long g_p3d_trace[4096 * 8];
+#define P3D_STAMP(k)                                                                             \
+  do {                                                                                           \
+    if ((threadIdx.x & 63) == 0 && (blockIdx.x + gridDim.x * blockIdx.y) < 4096)                 \
+      g_p3d_trace[(blockIdx.x + gridDim.x * blockIdx.y) * 8 + (k)] = wall_clock64();             \
+  } while (0)
+extern "C" int p3d_debug_trace(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p3d_trace), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : 2;
+}
+#else
+#define P3D_STAMP(k) do { } while (0)
+#endif
 
 // RS row tiles of 16 per wave; WK waves split the contraction; KIND only separates the
 // symbols of the input / hidden / output layers for rocprof.
@@ -62,6 +78,8 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   const bool cok = col < p.N;
   const int cc = cok ? col : p.N - 1;
   const int ngN = (p.N + 15) >> 4;
+  const bool trace = (RS == 4 && KIND == 1 && w == 0);
+  if (trace) P3D_STAMP(0);
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
   uint64_t ctr = p.ctr;
@@ -85,7 +103,9 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
   p3d_core<RS, DEPTH, NACC, APK>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
+  if (trace) P3D_STAMP(1);
   if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
+  if (trace) P3D_STAMP(2);
   // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r of column n0+i ---------------
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
   float z[RS][4];
@@ -94,6 +114,39 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) z[s][r] = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + b;
 
+  if (p.bn == 3) {
+    // BN-train, split form (k_bn_fwd finishes the layer): z and this row tile's per-column
+    // count-weighted moments {sum, M2 about the tile mean} for Chan's combination
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (m0 + 16 * s + 4 * q + r < p.M) sum += z[s][r];
+    sum = p3d_colsum16(sum);
+    const int nt = min(16 * RS, p.M - m0);
+    const float mt = sum / (float)nt;
+    float sq = 0.f;
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mt; sq += d * d; }
+    sq = p3d_colsum16(sq);
+    if (!cok) return;
+    if (q == 0) {
+      p.bnpart[((int64_t)blockIdx.y * p.N + col) * 2] = sum;
+      p.bnpart[((int64_t)blockIdx.y * p.N + col) * 2 + 1] = sq;
+    }
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 16 * s + 4 * q + r;
+        if (row < p.M) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
+      }
+    return;
+  }
   float inv = 1.0f, shift = 0.0f;
   if (p.bn) {
     float mean = mmu, var = mva;
@@ -124,6 +177,13 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     inv = (1.0f / sqrtf(var + p.eps)) * gam;
     shift = bet - mean * inv;
   }
+  if (trace) P3D_STAMP(3);
+  float uu[RS][4];
+  if (p.keep < 1.0f) {
+#pragma unroll
+    for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu[s]);
+  }
+  if (trace) P3D_STAMP(4);
   if (!cok) return;
 #pragma unroll
   for (int s = 0; s < RS; ++s)
@@ -134,14 +194,115 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       if (p.z_save) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
       float y = p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
-      if (p.keep < 1.0f) {
-        const float u = p3d_uniform(p.seed, ctr, p.site, p.row_off + row, col);
-        y = (y / p.keep) * p3d_dropout_mask(p.keep, u);
-      }
+      if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, uu[s][r]);
       if (p.res) y += rv[s][r];
       if (YPK) p.Y[p3d_pk(row, col, ngN)] = y;
       else p.Y[(int64_t)row * p.ldy + col] = y;
     }
+  if (trace) P3D_STAMP(5);
+}
+
+// =====================================================================================
+// BN-train forward, second half (split form): batch statistics from the row-tile moments,
+// then y = dropout(relu(BN(z))) (+ residual) on the packed layout: one 16x16 tile per
+// 64-lane workgroup, lane l holding row 16rt + (l&15), columns 16ct + 4(l>>4) .. +3, so
+// one float4 per operand and one Philox block per lane (its four dropout words).
+// TF1 semantics as k_fwd bn == 2 (biased variance, moving m -= (m - stat) * (1 - momentum)).
+// =====================================================================================
+struct BnFwdArgs {
+  const float* z; const float* part;   // packed [M, N]; [R][N][2]
+  int M, N;
+  const float* gamma; const float* beta;
+  float* mmean; float* mvar; float eps; float decay;
+  float* mean_save; float* var_save;
+  int relu;
+  float keep; uint64_t seed; uint64_t ctr; int site; int64_t row_off;
+  const int64_t* ctr_dev;
+  const float* res;                    // packed residual or null
+  float* Y;                            // packed [M, N]
+};
+
+// The <= 4 row-tile partial pairs of columns n0..n0+3 ([t][col][2] layout: 8 consecutive
+// floats per tile), all issued up front.
+__device__ __forceinline__ void p3d_load_parts(const float* part, int M, int N, int n0, f32x4 (&pp)[4][2]) {
+  const int R = (M + 15) >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int tt = t < R ? t : 0;
+    const f32x4* src = (const f32x4*)(part + ((int64_t)tt * N + n0) * 2);
+    pp[t][0] = src[0];
+    pp[t][1] = src[1];
+  }
+}
+
+__global__ __launch_bounds__(64) void k_bn_fwd(BnFwdArgs p) {
+  const int lane = threadIdx.x, ct = blockIdx.x, rt = blockIdx.y;
+  const int j = lane & 15, q = lane >> 4;
+  const int n0 = 16 * ct + 4 * q, row = 16 * rt + j;
+  const int ngN = p.N >> 4;
+  const int R = (p.M + 15) >> 4;
+  const int64_t off = ((int64_t)rt * ngN + ct) * 256 + lane * 4;
+  // every operand load issued before any arithmetic
+  f32x4 pp[4][2];
+  p3d_load_parts(p.part, p.M, p.N, n0, pp);
+  const f32x4 z4 = *(const f32x4*)(p.z + off);
+  const f32x4 g4 = *(const f32x4*)(p.gamma + n0), b4 = *(const f32x4*)(p.beta + n0);
+  f32x4 r4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (p.res) r4 = *(const f32x4*)(p.res + off);
+  f32x4 mm4 = f32x4{0.f, 0.f, 0.f, 0.f}, mv4 = mm4;
+  const bool owner = (rt == 0 && j == 0);
+  if (owner) { mm4 = *(const f32x4*)(p.mmean + n0); mv4 = *(const f32x4*)(p.mvar + n0); }
+  const uint64_t ctr = p.ctr_dev ? (uint64_t)*p.ctr_dev : p.ctr;
+  float u[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.keep < 1.0f) {
+    const uint4 wq = p3d_philox(make_uint4((uint32_t)(p.row_off + row), (uint32_t)(n0 >> 2), (uint32_t)p.site,
+                                           (uint32_t)ctr), (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+    const uint32_t xs[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) u[e] = __uint_as_float((xs[e] & 0x7FFFFFu) | 0x3F800000u) - 1.0f;
+  }
+  const float fm = (float)p.M;
+  f32x4 o, mean4, var4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    // element e of column n0+e sits at float 2e (sum) / 2e+1 (M2) of the tile's 8 floats
+    float S = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < R) S += pp[t][e >> 1][(e & 1) * 2];
+    const float mean = S / fm;
+    float M2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < R) {
+        const int nt = min(16, p.M - 16 * t);
+        const float d = pp[t][e >> 1][(e & 1) * 2] / (float)nt - mean;
+        M2 += pp[t][e >> 1][(e & 1) * 2 + 1] + (float)nt * d * d;
+      }
+    const float var = M2 / fm;
+    mean4[e] = mean;
+    var4[e] = var;
+    const float inv = (1.0f / sqrtf(var + p.eps)) * g4[e];
+    const float shift = b4[e] - mean * inv;
+    float y = z4[e] * inv + shift;
+    if (p.relu) y = fmaxf(y, 0.0f);
+    if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, u[e]);
+    if (p.res) y += r4[e];
+    o[e] = row < p.M ? y : 0.0f;
+  }
+  *(f32x4*)(p.Y + off) = o;
+  if (owner) {
+    *(f32x4*)(p.mean_save + n0) = mean4;
+    *(f32x4*)(p.var_save + n0) = var4;
+    f32x4 nm, nv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      nm[e] = mm4[e] - (mm4[e] - mean4[e]) * p.decay;
+      nv[e] = mv4[e] - (mv4[e] - var4[e]) * p.decay;
+    }
+    *(f32x4*)(p.mmean + n0) = nm;
+    *(f32x4*)(p.mvar + n0) = nv;
+  }
 }
 
 // =====================================================================================
@@ -162,15 +323,18 @@ struct BwdArgs {
   const int64_t* ctr_dev;
   float* dz;                      // packed [M, K]: gradient wrt prev layer's z
   float* dgamma; float* dbeta;    // [K]
+  float* bnpart;                  // split BN backward: per (row tile, column) {sum g, sum g*xhat};
+                                  // dz then holds g (k_bn_bwd finishes it)
 };
 
-template <int WK, int DEPTH, int NACC, bool APK, int KIND>
+// RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
+// RS = 1: 16x16 tiles over a (K/16, M/16) grid, BN sums left as row-tile partials (bnpart).
+template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
 __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
-  constexpr int RS = 4;
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int ct = blockIdx.x, n0 = ct * 16;
+  const int ct = blockIdx.x, n0 = ct * 16, m0 = blockIdx.y * 16 * RS;
   const int col = n0 + i;
   const bool cok = col < p.K;
   const int cc = cok ? col : p.K - 1;
@@ -185,7 +349,7 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
     for (int s = 0; s < RS; ++s)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * s + 4 * q + r;
+        const int row = m0 + 16 * s + 4 * q + r;
         zz[s][r] = p.prev ? p.z[p3d_pk(row, cc, ngK)] : 0.f;
         dr[s][r] = p.dres ? p.dres[p3d_pk(row, cc, ngK)] : 0.f;
       }
@@ -197,7 +361,7 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   for (int a = 0; a < NACC; ++a)
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, 0, p.Wd, ngt, ct, gb, ge, acc);
+  p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, m0, p.Wd, ngt, ct, gb, ge, acc);
   if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
   float g[RS][4];
@@ -205,7 +369,7 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   for (int s = 0; s < RS; ++s)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = 16 * s + 4 * q + r;
+      const int row = m0 + 16 * s + 4 * q + r;
       const float d = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + dr[s][r];
       if (p.draw && cok && row < p.M) p.draw[p3d_pk(row, col, ngK)] = d;
       g[s][r] = d;
@@ -220,17 +384,19 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   }
   float xh[RS][4];
   float sg = 0.f, sgx = 0.f;
+  float uu[RS][4];
+  if (p.keep < 1.0f) {
+#pragma unroll
+    for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu[s]);
+  }
 #pragma unroll
   for (int s = 0; s < RS; ++s)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = 16 * s + 4 * q + r;
+      const int row = m0 + 16 * s + 4 * q + r;
       const bool ok = row < p.M;
       float gg = g[s][r];
-      if (p.keep < 1.0f) {
-        const float u = p3d_uniform(p.seed, ctr, p.site, p.row_off + row, cc);
-        gg = (gg * p3d_dropout_mask(p.keep, u)) / p.keep;
-      }
+      if (p.keep < 1.0f) gg = (gg * p3d_dropout_mask(p.keep, uu[s][r])) / p.keep;
       const float a = p.bn ? zz[s][r] * inv + shift : zz[s][r];
       if (p.relu && !(a > 0.0f)) gg = 0.0f;
       if (!ok) gg = 0.0f;
@@ -243,6 +409,21 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   if (p.bn) {
     sg = p3d_colsum16(sg);
     sgx = p3d_colsum16(sgx);
+    if (p.bnpart) {   // split form: partials + g; k_bn_bwd forms dz, dgamma, dbeta
+      if (!cok) return;
+      if (q == 0) {
+        p.bnpart[((int64_t)blockIdx.y * p.K + col) * 2] = sg;
+        p.bnpart[((int64_t)blockIdx.y * p.K + col) * 2 + 1] = sgx;
+      }
+#pragma unroll
+      for (int s = 0; s < RS; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + 16 * s + 4 * q + r;
+          if (row < p.M) p.dz[p3d_pk(row, col, ngK)] = g[s][r];
+        }
+      return;
+    }
     if (q == 0 && cok) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
   }
   if (!cok) return;
@@ -251,11 +432,60 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   for (int s = 0; s < RS; ++s)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = 16 * s + 4 * q + r;
+      const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
       const float dz = p.bn ? (inv / fm) * (fm * g[s][r] - sg - xh[s][r] * sgx) : g[s][r];
       p.dz[p3d_pk(row, col, ngK)] = dz;
     }
+}
+
+// =====================================================================================
+// BN-train backward, second half (split form): dz = inv/M * (M g - sum g - xhat sum g*xhat)
+// from the row-tile partials, in place over g (packed), dgamma = sum g*xhat, dbeta = sum g.
+// =====================================================================================
+struct BnBwdArgs {
+  float* dz; const float* z; const float* part;   // dz holds g on entry; [R][K][2]
+  int M, K;
+  const float* mean; const float* var; const float* gamma; float eps;
+  float* dgamma; float* dbeta;
+};
+
+__global__ __launch_bounds__(64) void k_bn_bwd(BnBwdArgs p) {
+  const int lane = threadIdx.x, ct = blockIdx.x, rt = blockIdx.y;
+  const int j = lane & 15, q = lane >> 4;
+  const int n0 = 16 * ct + 4 * q, row = 16 * rt + j;
+  const int ngK = p.K >> 4;
+  const int R = (p.M + 15) >> 4;
+  const int64_t off = ((int64_t)rt * ngK + ct) * 256 + lane * 4;
+  f32x4 pp[4][2];
+  p3d_load_parts(p.part, p.M, p.K, n0, pp);
+  const f32x4 g4 = *(const f32x4*)(p.dz + off);
+  const f32x4 z4 = *(const f32x4*)(p.z + off);
+  const f32x4 mu4 = *(const f32x4*)(p.mean + n0), va4 = *(const f32x4*)(p.var + n0);
+  const f32x4 ga4 = *(const f32x4*)(p.gamma + n0);
+  const float fm = (float)p.M;
+  f32x4 o, sg4, sgx4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < R) {
+        sg += pp[t][e >> 1][(e & 1) * 2];
+        sgx += pp[t][e >> 1][(e & 1) * 2 + 1];
+      }
+    sg4[e] = sg;
+    sgx4[e] = sgx;
+    const float rstd = 1.0f / sqrtf(va4[e] + p.eps);
+    const float inv = rstd * ga4[e];
+    const float xh = (z4[e] - mu4[e]) * rstd;
+    o[e] = row < p.M ? (inv / fm) * (fm * g4[e] - sg - xh * sgx) : 0.0f;
+  }
+  *(f32x4*)(p.dz + off) = o;
+  if (rt == 0 && j == 0) {
+    *(f32x4*)(p.dgamma + n0) = sgx4;
+    *(f32x4*)(p.dbeta + n0) = sg4;
+  }
 }
 
 // =====================================================================================
@@ -668,6 +898,8 @@ struct p3d_model {
   float* wpk = nullptr;       // packed weights (Wf, Wd per layer)
   float* ws = nullptr;        // activation workspace
   float* scratch = nullptr;   // reductions (max-norm)
+  float* bnpart = nullptr;    // inside scratch: split BN-train row-tile partials
+  int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
   float* aff = nullptr;             // BN-eval affine per BN layer
@@ -699,6 +931,7 @@ struct p3d_model {
   // workgroups co-reside per CU, so independent batches on different streams overlap
   // (tools/streams_sweep2.py: 4 streams 5.6 M poses/s vs 4.9 M with 16-wave workgroups).
   int infer_wk = 8;
+  int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -902,10 +1135,12 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   m->dout[0] = cur; cur += pad64(Bp * L);
   m->dout[1] = cur; cur += pad64(Bp * L);
-  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64;
+  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + 4 * 2 * (int64_t)L;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev) == 8 ? 8 : 16;
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
+  if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
+  if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   {
     StepState s0{};
@@ -915,6 +1150,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
   m->gw = m->wsq + 64;
+  m->bnpart = m->gw + 64;   // [4 row tiles][L][2]: split BN-train partial moments / sums
   // TF defaults: BN gamma = 1, moving_variance = 1 (beta/mean = 0 already)
   if (c.batch_norm) {
     std::vector<float> ones(L, 1.0f);
@@ -1041,7 +1277,8 @@ template <bool APK, bool YPK, int KIND>
 static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch, int wk, hipStream_t st) {
   const int gx = (a.N + 15) / 16;
   if (whole_batch) {
-    go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
+    if (wk == 16) go(ps, k_fwd<4, 16, 4, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(1024), st, a);
+    else go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
   } else {
     const int gy = (a.M + 15) / 16;
     if (wk == 8) go(ps, k_fwd<1, 8, 8, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
@@ -1072,6 +1309,33 @@ static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
   else go(ps, k_gemm_f32<1, 4>, dim3(grid), dim3(256), st, g);
 }
 
+// BN-train layer, split form: 16x16 GEMM tiles (256 workgroups at L = 1024, B = 64) write z
+// and row-tile moments, then k_bn_fwd applies batch-stat BN / ReLU / dropout / residual.
+static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
+  FwdArgs a = a0;
+  a.bn = 3; a.bnpart = m->bnpart;
+  const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
+  {
+    static const char* tags[3] = {"fwd_in_train_z", "fwd_hidden_train_z", "fwd_out_train_z"};
+    ProfScope ps(m, tags[kind]);
+    if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, grid, dim3(512), st, a);
+    else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, grid, dim3(512), st, a);
+  }
+  LAUNCH_CHECK("k_fwd");
+  BnFwdArgs b{};
+  b.z = a.z_save; b.part = m->bnpart; b.M = a.M; b.N = a.N;
+  b.gamma = a.gamma; b.beta = a.beta; b.mmean = a.mmean; b.mvar = a.mvar; b.eps = a.eps; b.decay = a.decay;
+  b.mean_save = a.mean_save; b.var_save = a.var_save;
+  b.relu = a.relu; b.keep = a.keep; b.seed = a.seed; b.ctr = a.ctr; b.site = a.site; b.row_off = a.row_off;
+  b.ctr_dev = a.ctr_dev; b.res = a.res; b.Y = a.Y;
+  {
+    ProfScope ps(m, "bn_fwd");
+    go(ps, k_bn_fwd, grid, dim3(64), st, b);
+  }
+  LAUNCH_CHECK("k_bn_fwd");
+  return P3D_OK;
+}
+
 static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch, hipStream_t st) {
   if (use_big(m, a, kind, whole_batch)) {
     launch_big(m, a, st);
@@ -1088,9 +1352,10 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind]);
-  if (kind == 0) launch_fwd_k<false, true, 0>(ps, a, whole_batch, m->infer_wk, st);
-  else if (kind == 1) launch_fwd_k<true, true, 1>(ps, a, whole_batch, m->infer_wk, st);
-  else launch_fwd_k<true, false, 2>(ps, a, whole_batch, m->infer_wk, st);
+  const int wk = whole_batch ? m->train_wk : m->infer_wk;
+  if (kind == 0) launch_fwd_k<false, true, 0>(ps, a, whole_batch, wk, st);
+  else if (kind == 1) launch_fwd_k<true, true, 1>(ps, a, whole_batch, wk, st);
+  else launch_fwd_k<true, false, 2>(ps, a, whole_batch, wk, st);
   LAUNCH_CHECK("k_fwd");
   return P3D_OK;
 }
@@ -1209,6 +1474,12 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
     if (last) { a.Y = y; a.ldy = ly.N; }
     else { a.Y = m->act[l] + wsoff; a.ldy = 0; }
     const int kind = (l == 0) ? 0 : (last ? 2 : 1);
+    if (training && ly.bn && m->train_split) {
+      const int rc = launch_fwd_split(m, a, kind, st);
+      if (rc) return rc;
+      in = a.Y;
+      continue;
+    }
     const int rc = launch_fwd(m, a, kind, training && ly.bn, st);
     if (rc) return rc;
     in = a.Y;
@@ -1332,13 +1603,38 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     a.ctr_dev = m->ctr_dev;
     a.dz = m->dz[l - 1];
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
-    {
-      ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
-      const dim3 grid((a.K + 15) / 16, 1);
-      if (dz_pk) go(ps, k_dgrad<8, 8, 2, true, 1>, grid, dim3(512), st, a);
-      else go(ps, k_dgrad<8, 8, 2, false, 2>, grid, dim3(512), st, a);
+    if (m->train_split) {
+      if (pv.bn) a.bnpart = m->bnpart;
+      const dim3 grid((a.K + 15) / 16, (a.M + 15) / 16);
+      {
+        ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
+        if (dz_pk) go(ps, k_dgrad<1, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
+        else go(ps, k_dgrad<1, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
+      }
+      LAUNCH_CHECK("k_dgrad");
+      if (pv.bn) {
+        BnBwdArgs b{};
+        b.dz = a.dz; b.z = a.z; b.part = m->bnpart; b.M = a.M; b.K = a.K;
+        b.mean = a.mean; b.var = a.var; b.gamma = a.gamma; b.eps = a.eps;
+        b.dgamma = a.dgamma; b.dbeta = a.dbeta;
+        ProfScope ps(m, "bn_bwd");
+        go(ps, k_bn_bwd, grid, dim3(64), st, b);
+        LAUNCH_CHECK("k_bn_bwd");
+      }
+    } else {
+      {
+        ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
+        const dim3 grid((a.K + 15) / 16, 1);
+        if (m->train_wk == 16) {
+          if (dz_pk) go(ps, k_dgrad<4, 16, 4, 2, true, 1>, grid, dim3(1024), st, a);
+          else go(ps, k_dgrad<4, 16, 4, 2, false, 2>, grid, dim3(1024), st, a);
+        } else {
+          if (dz_pk) go(ps, k_dgrad<4, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
+          else go(ps, k_dgrad<4, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
+        }
+      }
+      LAUNCH_CHECK("k_dgrad");
     }
-    LAUNCH_CHECK("k_dgrad");
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
     dz_cur = m->dz[l - 1];
     dz_pk = true;

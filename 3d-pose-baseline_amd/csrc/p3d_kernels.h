@@ -49,6 +49,28 @@ __device__ __forceinline__ float p3d_uniform(uint64_t seed, uint64_t ctr, int si
   return __uint_as_float((x & 0x7FFFFFu) | 0x3F800000u) - 1.0f;
 }
 
+// The uniforms of rows row0 .. row0+3 of this lane's column `col` (u[r] = p3d_uniform(..,
+// row0 + r, col)) in the MFMA C layout, where lane i + 16q holds column n0 + i and rows
+// 4q + r: one Philox block per lane instead of four.  Lane 4a + j computes the block of
+// (row0 + j, col >> 2), whose four words are the four columns of its lane quad; four
+// rotations through ds_bpermute hand every lane its own column's word of all four rows.
+// Requires the 4 lanes of a quad to share col >> 2 (n0 a multiple of 4) and row0 to be
+// uniform over each 16-lane group.  All 64 lanes must execute it.
+__device__ __forceinline__ void p3d_uniform_rows4(uint64_t seed, uint64_t ctr, int site, int64_t row0, int col,
+                                                  float u[4]) {
+  const int lane = threadIdx.x & 63;
+  const uint4 w = p3d_philox(make_uint4((uint32_t)(row0 + (lane & 3)), (uint32_t)(col >> 2), (uint32_t)site,
+                                        (uint32_t)ctr), (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int c = (lane - t) & 3;                       // the word my quad-mate wants from me
+    const uint32_t give = c == 0 ? w.x : c == 1 ? w.y : c == 2 ? w.z : w.w;
+    const int src = (lane & ~3) + ((lane + t) & 3);
+    const uint32_t got = (uint32_t)__shfl((int)give, src, 64);
+    u[(lane + t) & 3] = __uint_as_float((got & 0x7FFFFFu) | 0x3F800000u) - 1.0f;
+  }
+}
+
 // tf.nn.dropout (TF1): binary = floor(keep + U); y = x / keep * binary
 __device__ __forceinline__ float p3d_dropout_mask(float keep, float u) { return floorf(keep + u); }
 

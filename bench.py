@@ -270,7 +270,7 @@ def bench_train(args, rank, world, steps=None, warmup=None):
 
     def run(k):
         for i in range(k):
-            model.train_step_device(X[i % G], T[i % G], 0.5, out=Y)
+            model.train_step_device(X[i % G], T[i % G], args.keep, out=Y)
 
     use_graph = world == 1 or args.train_graph
     run(max(2, warmup // 4))
@@ -456,6 +456,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
     ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
+    ap.add_argument("--keep", type=float, default=0.5, help="dropout keep_prob of the train step")
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")

@@ -129,7 +129,11 @@ def test_gradients_variants(residual, batch_norm, max_norm, B):
                             max_norm=max_norm), 0.5, B)
 
 
-def test_train_steps_track_oracle():
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_train_steps_track_oracle(split, monkeypatch):
+    """5 TF1 train steps vs the oracle.  split=1: BN-train layers as 16x16-tile GEMM +
+    k_bn_fwd / k_bn_bwd (default); split=0: whole-batch-per-workgroup kernels."""
+    monkeypatch.setenv("P3D_TRAIN_SPLIT", split)
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     st, m = make(cfg, lr=1e-3)
     rng = np.random.default_rng(21)

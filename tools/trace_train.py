@@ -1,0 +1,37 @@
+"""Phase timestamps of the BN-train hidden forward kernel (dev tool).
+
+Needs the tracing build:  hipcc ... -DP3D_TRACE -o 3d-pose-baseline_amd/libp3d_trace.so
+    P3D_LIB=$PWD/3d-pose-baseline_amd/libp3d_trace.so python tools/trace_train.py [keep]
+Prints, per phase, the min/median/max over workgroups of the wall_clock64 (100 MHz) delta
+from the earliest workgroup start of the last traced launch.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import _p3d  # noqa: E402
+
+keep = float(sys.argv[1]) if len(sys.argv) > 1 else 0.5
+model, _ = bench.make_model()
+X = torch.randn(64, 32, device="cuda")
+T = torch.randn(64, 48, device="cuda")
+for _ in range(20):
+    model.train_step_device(X, T, keep)
+torch.cuda.synchronize()
+lib = _p3d.lib()
+lib.p3d_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros(4096 * 8, np.uint64)
+assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
+t = buf.reshape(4096, 8)[:64, :6].astype(np.int64)   # 64 workgroups of the RS=4 launch
+t0 = t[:, 0].min()
+names = ["start", "gemm(w0)", "reduced", "bn", "philox", "stored"]
+for k, n in enumerate(names):
+    d = (t[:, k] - t0) * 10.0 / 1000.0
+    print("%-9s min %6.2f  med %6.2f  max %6.2f us" % (n, d.min(), np.median(d), d.max()))
