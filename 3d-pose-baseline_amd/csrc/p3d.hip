@@ -538,7 +538,9 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
   f32x4 acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbs = 0.f;
+  __shared__ float dbp[4][64];
+  const bool do_db = p.db && blockIdx.y == 0;
+  float dbs = 0.f;   // wave w: rows 16w .. 16w+15 of column `lane` (summed in row order)
   for (int mc = 0; mc < p.M; mc += 64) {
     p3d_stage64(xs, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
     p3d_stage64(zs, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
@@ -551,12 +553,20 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
       for (int s = 0; s < 4; ++s)
         acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[m * WG_LDS_STRIDE + 16 * s + i], acc[s], 0, 0, 0);
     }
-    if (p.db && blockIdx.y == 0 && tid < 64) {
-      for (int m = 0; m < 64; ++m) dbs += zs[m * WG_LDS_STRIDE + tid];
+    if (do_db) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = zs[(16 * w + r) * WG_LDS_STRIDE + lane];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dbs += v[r];
     }
     __syncthreads();
   }
-  if (p.db && blockIdx.y == 0 && tid < 64 && n0 + tid < p.N) p.db[n0 + tid] = dbs;
+  if (do_db) {
+    dbp[w][lane] = dbs;
+    __syncthreads();
+    if (w == 0 && n0 + lane < p.N) p.db[n0 + lane] = ((dbp[0][lane] + dbp[1][lane]) + dbp[2][lane]) + dbp[3][lane];
+  }
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
