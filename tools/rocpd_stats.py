@@ -33,3 +33,18 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def roofline_phase_csv(trace_csv, symbol, graph_streams_min=2):
+    """From a --kernel-trace CSV of bench.py's default run: durations (ns) of the launches of
+    `symbol` on the model's own stream that follow the last graph replay (the roofline phase:
+    20 warm-up + 200 back-to-back + 200 event-timed launches), in order."""
+    rows = sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
+    ks = [r for r in rows if symbol in r["Kernel_Name"]]
+    from collections import Counter
+    cnt = Counter(r["Stream_Id"] for r in ks)
+    own = [s for s, _ in cnt.most_common() if s == "0"] or [cnt.most_common()[-1][0]]
+    graph_streams = {s for s in cnt if s not in own}
+    last_graph = max(int(r["Start_Timestamp"]) for r in ks if r["Stream_Id"] in graph_streams)
+    return [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ks
+            if r["Stream_Id"] in own and int(r["Start_Timestamp"]) > last_graph]
