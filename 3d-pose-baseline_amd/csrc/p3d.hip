@@ -940,7 +940,8 @@ struct p3d_model {
   // waves per inference workgroup (P3D_INFER_WK = 8 | 16).  8 waves x 94 VGPRs lets two
   // workgroups co-reside per CU, so independent batches on different streams overlap
   // (tools/streams_sweep2.py: 4 streams 5.6 M poses/s vs 4.9 M with 16-wave workgroups).
-  int infer_wk = 8;
+  int infer_wk = 82;        // inference tiling variant (launch_fwd_k), env P3D_INFER_WK
+  int in_wk = 2, out_wk = 16; // input / output layer variants (env P3D_IN_WK, P3D_OUT_WK; 0 = infer_wk)
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
@@ -1147,7 +1148,9 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   m->dout[1] = cur; cur += pad64(Bp * L);
   const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + 4 * 2 * (int64_t)L;
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
-  if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev) == 8 ? 8 : 16;
+  if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
@@ -1290,8 +1293,19 @@ static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch
     if (wk == 16) go(ps, k_fwd<4, 16, 4, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(1024), st, a);
     else go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
   } else {
-    const int gy = (a.M + 15) / 16;
+    // tiling variants (P3D_INFER_WK): 8 = 1 row tile x 8 waves (default), 16 = 16 waves,
+    // 84 = 8 waves with a 4-group register ring, 28 = 2 row tiles x 8 waves, 216 = 2 x 16
+    const int gy = (a.M + 15) / 16, gy2 = (a.M + 31) / 32;
     if (wk == 8) go(ps, k_fwd<1, 8, 8, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 84) go(ps, k_fwd<1, 8, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 82) go(ps, k_fwd<1, 8, 2, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 80) go(ps, k_fwd<1, 8, 1, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 83) go(ps, k_fwd<1, 8, 2, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 81) go(ps, k_fwd<1, 8, 4, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 44) go(ps, k_fwd<1, 4, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(256), st, a);
+    else if (wk == 162) go(ps, k_fwd<1, 16, 2, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(1024), st, a);
+    else if (wk == 28) go(ps, k_fwd<2, 8, 4, 2, APK, YPK, KIND>, dim3(gx, gy2), dim3(512), st, a);
+    else if (wk == 216) go(ps, k_fwd<2, 16, 2, 2, APK, YPK, KIND>, dim3(gx, gy2), dim3(1024), st, a);
     else go(ps, k_fwd<1, 16, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(1024), st, a);
   }
 }
@@ -1362,7 +1376,14 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   static const char* tags[2][3] = {{"fwd_in", "fwd_hidden", "fwd_out"},
                                    {"fwd_in_train", "fwd_hidden_train", "fwd_out_train"}};
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind]);
-  const int wk = whole_batch ? m->train_wk : m->infer_wk;
+  int wk = whole_batch ? m->train_wk : m->infer_wk;
+  if (!whole_batch && kind == 0 && m->in_wk) wk = m->in_wk;
+  if (!whole_batch && kind == 2 && m->out_wk) wk = m->out_wk;
+  if (kind == 0 && wk == 2) {   // K = 32: one k-group per wave
+    go(ps, k_fwd<1, 2, 1, 2, false, true, 0>, dim3((a.N + 15) / 16, (a.M + 15) / 16), dim3(128), st, a);
+    LAUNCH_CHECK("k_fwd");
+    return P3D_OK;
+  }
   if (kind == 0) launch_fwd_k<false, true, 0>(ps, a, whole_batch, wk, st);
   else if (kind == 1) launch_fwd_k<true, true, 1>(ps, a, whole_batch, wk, st);
   else launch_fwd_k<true, false, 2>(ps, a, whole_batch, wk, st);

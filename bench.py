@@ -160,9 +160,12 @@ def bench_infer(args, rank, world):
     import torch
     S = args.streams
     model, _ = make_model(data_parallel=False, max_batch=BATCH * S)
-    G = args.graph_steps
-    while args.steps % G or G % S:
-        G -= 1
+    # R replay rounds of G = K / R steps (G <= --graph-steps), the G steps of a round split
+    # over the S streams as evenly as possible: exactly K timed steps for any K and S
+    R = max(1, -(-args.steps // args.graph_steps))
+    while args.steps % R:
+        R += 1
+    G = args.steps // R
     rng = np.random.default_rng(100 + rank)
     X = torch.from_numpy(rng.standard_normal((G, BATCH, IN)).astype(np.float32)).cuda()
     Y = torch.empty((G, BATCH, OUT), dtype=torch.float32, device="cuda")
@@ -175,7 +178,7 @@ def bench_infer(args, rank, world):
     # round robin; the first pool streams share queues with torch's own, so one round of
     # streams is touched first and the batch streams land on 4 distinct idle queues
     # (tools/streams_probe.py: 3.8 -> 5.6 M poses/s at 4 streams).
-    spare = [torch.cuda.Stream() for _ in range(4)]
+    spare = [torch.cuda.Stream() for _ in range(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))]
     for st in spare:
         with torch.cuda.stream(st):
             torch.zeros(16, device="cuda").add_(1)
@@ -183,13 +186,13 @@ def bench_infer(args, rank, world):
 
     def capture(nstreams):
         streams = [torch.cuda.Stream() for _ in range(nstreams)]
-        per = G // nstreams
+        counts = [G // nstreams + (1 if j < G % nstreams else 0) for j in range(nstreams)]
+        first = [sum(counts[:j]) for j in range(nstreams)]
         graphs = []
         for j, st in enumerate(streams):
             def body(j=j):
-                for i in range(per):
-                    model.forward_device(X[j * per + i], False, 1.0, out=Y[j * per + i], ctr=0,
-                                         ws_row=BATCH * j)
+                for i in range(first[j], first[j] + counts[j]):
+                    model.forward_device(X[i], False, 1.0, out=Y[i], ctr=0, ws_row=BATCH * j)
             with torch.cuda.stream(st):
                 body()
             torch.cuda.synchronize()
@@ -210,7 +213,7 @@ def bench_infer(args, rank, world):
             fn()
         barrier_sync(world)
         t0 = time.perf_counter()
-        for _ in range(steps // G):
+        for _ in range(R):
             fn()
         barrier_sync(world)
         return max_over_ranks(time.perf_counter() - t0, world)
@@ -528,4 +531,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        # report and leave without interpreter teardown: unwinding with live HIP graphs and
+        # streams after an exception has crashed the process (SIGSEGV) on the box
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)
