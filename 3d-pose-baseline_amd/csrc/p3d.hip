@@ -1762,6 +1762,38 @@ extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const dou
   return p3d_mpjpe_accum_ex(pred_n, gt_n, 48, mean96, std96, dims48, B, 17, 0, joint_sum17, nullptr, stream);
 }
 
+// rocprofv3 name of the kernel a launch of `what` uses under the current tiling variants:
+// 0 = inference hidden layer at B <= 64 (bench.py's roofline kernel), 1 = inference hidden
+// layer at large M, 2 = BN-train hidden GEMM.
+extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len) {
+  if (!m || !out || out_len <= 0) return fail(P3D_ERR_ARG, "p3d_kernel_name: bad argument");
+  std::string n;
+  if (what == 0) {
+    switch (m->infer_wk) {
+      case 8: n = "k_fwd<1, 8, 8, 2, true, true, 1>"; break;
+      case 84: n = "k_fwd<1, 8, 4, 2, true, true, 1>"; break;
+      case 82: n = "k_fwd<1, 8, 2, 2, true, true, 1>"; break;
+      case 80: n = "k_fwd<1, 8, 1, 2, true, true, 1>"; break;
+      case 83: n = "k_fwd<1, 8, 2, 1, true, true, 1>"; break;
+      case 81: n = "k_fwd<1, 8, 4, 1, true, true, 1>"; break;
+      case 44: n = "k_fwd<1, 4, 4, 2, true, true, 1>"; break;
+      case 162: n = "k_fwd<1, 16, 2, 2, true, true, 1>"; break;
+      case 28: n = "k_fwd<2, 8, 4, 2, true, true, 1>"; break;
+      case 216: n = "k_fwd<2, 16, 2, 2, true, true, 1>"; break;
+      default: n = "k_fwd<1, 16, 4, 2, true, true, 1>"; break;
+    }
+  } else if (what == 1) {
+    n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
+  } else if (what == 2) {
+    n = m->train_split ? "k_fwd<1, 8, 8, 2, true, true, 1>" : "k_fwd<4, 8, 8, 2, true, true, 1>";
+  } else {
+    return fail(P3D_ERR_ARG, "p3d_kernel_name: unknown kernel selector");
+  }
+  strncpy(out, n.c_str(), (size_t)out_len - 1);
+  out[out_len - 1] = 0;
+  return P3D_OK;
+}
+
 extern "C" int p3d_profile_start(p3d_model* m, int32_t max_launches) {
   if (!m || max_launches <= 0) return fail(P3D_ERR_ARG, "p3d_profile_start: bad argument");
   for (auto e : m->ev) (void)hipEventDestroy(e);

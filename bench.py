@@ -52,10 +52,17 @@ def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # P3D_BENCH_BACKEND=gloo (+ P3D_BENCH_DEVICE=0): rehearse the N-rank path with several
+    # ranks sharing one GPU (RCCL refuses two ranks on one device); the product path is nccl
+    backend = os.environ.get("P3D_BENCH_BACKEND", "nccl")
+    dev = int(os.environ.get("P3D_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, local
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, dev
 
 
 def barrier_sync(world):
@@ -71,7 +78,7 @@ def max_over_ranks(x, world):
     import torch.distributed as dist
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -107,6 +114,15 @@ def profile_kernels(model, fn, n_launch_max=4096):
         tag, cnt, tot, mn, mx = line.split("\t")
         out[tag] = (int(cnt), float(tot) / int(cnt), float(mn), float(mx))
     return out
+
+
+def kernel_name(model, what):
+    """rocprof name of the kernel the library launches for `what` (p3d_kernel_name)."""
+    import ctypes
+    import _p3d
+    buf = ctypes.create_string_buffer(256)
+    _p3d.check(_p3d.lib().p3d_kernel_name(model._h, what, buf, len(buf)), "p3d_kernel_name")
+    return buf.value.decode()
 
 
 def _committed_traffic(symbol):
@@ -244,10 +260,11 @@ def bench_infer(args, rank, world):
     prof = profile_kernels(model, lambda: steps_eager(min(args.steps, 100)))
     flop = 2.0 * BATCH * L * L          # one hidden-layer launch: [64,1024] x [1024,1024]
     achieved = flop / (avg_us * 1e-6) / 1e12
-    traffic = args.traffic if args.traffic is not None else _committed_traffic("k_fwd<1, 8, 8, 2, true, true, 1>")
+    kname = kernel_name(model, 0)
+    traffic = args.traffic if args.traffic is not None else _committed_traffic(kname)
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-            "kernel": "k_fwd<1,8,8,2,true,true,1> (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
+            "kernel": kname + " (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
             "b2b_avg_us": round(b2b_us, 3), "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
     model.close()
@@ -381,7 +398,8 @@ def bench_eval(args, rank, world):
     flop = 2.0 * chunk * L * L
     roof = {"bound": "mfma", "achieved": round(flop / (avg_us * 1e-6) / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flop / (avg_us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "kernel": "k_gemm_f32<2> (hidden layer, 128x128 tiles)" if tag == "fwd_hidden_big" else "k_fwd",
+            "kernel": kernel_name(model, 1 if tag == "fwd_hidden_big" else 0) + " (hidden layer, M = %d)" % chunk,
+            "traffic": _committed_traffic(kernel_name(model, 1 if tag == "fwd_hidden_big" else 0)),
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3)}
     model.close()
     return {"workload": "cfg4 evaluateActionWise sweep: 15 actions, %d frames (tail-dropped), %s, "
@@ -440,8 +458,8 @@ def bench_stress(args, rank, world):
     flop = 2.0 * Bs * Ls * Ls
     achieved = flop / (avg_us * 1e-6) / 1e12
     roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16<64>"),
-            "kernel": "k_gemm_bf16<64> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16<64, 4>"),
+            "kernel": "k_gemm_bf16<64, 4> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps}
     model.close()
     return value, dt, roof, steps

@@ -149,6 +149,11 @@ int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const 
                        const double* std96, const int32_t* dims, int64_t B, int32_t n_joints,
                        int32_t procrustes, double* joint_sum, double* sq_sum, void* stream);
 
+/* rocprofv3 name of the kernel used for `what` under the model's tiling variants:
+ * 0 = inference hidden layer at B <= 64, 1 = inference hidden layer at large M,
+ * 2 = BN-train hidden-layer GEMM.  (Measurement plumbing for bench.py.) */
+int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len);
+
 /* Live kernel timing (bench.py's roofline): while active, every kernel the model
  * launches is bracketed by a hipEvent pair.  p3d_profile_stop synchronises and writes
  * one line per kernel tag: "tag\tcount\ttotal_us\tmin_us\tmax_us\n". */
