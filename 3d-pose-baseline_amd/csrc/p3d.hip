@@ -915,7 +915,7 @@ struct p3d_model {
   float* aff = nullptr;             // BN-eval affine per BN layer
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
-  int bf16_stages = 4;              // LDS ring depth of the hidden bf16 GEMM (P3D_BF16_STAGES)
+  int bf16_stages = 48;             // hidden bf16 GEMM variant (launch_bf16_layer; env P3D_BF16_STAGES)
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
@@ -1412,6 +1412,14 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
     if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 32) go(ps, k_gemm_bf16p<64, 3, 4>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 42) go(ps, k_gemm_bf16p<64, 4, 4>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 22) go(ps, k_gemm_bf16p<128, 2, 4>, dim3(grid), dim3(256), st, a);
+    else if (m->bf16_stages == 38) go(ps, k_gemm_bf16p<64, 3, 8>, dim3(grid), dim3(512), st, a);
+    else if (m->bf16_stages == 28) go(ps, k_gemm_bf16p<128, 2, 8>, dim3(grid), dim3(512), st, a);
+    else if (m->bf16_stages == 48) go(ps, k_gemm_bf16p<64, 4, 8>, dim3(grid), dim3(512), st, a);
+    else if (m->bf16_stages == 49) go(ps, k_gemm_bf16p<64, 4, 8, true>, dim3(grid), dim3(512), st, a);
+    else if (m->bf16_stages == 39) go(ps, k_gemm_bf16p<64, 3, 8, true>, dim3(grid), dim3(512), st, a);
     else if (m->bf16_stages == 2) go(ps, k_gemm_bf16<64, 2>, dim3(grid), dim3(256), st, a);
     else if (m->bf16_stages == 3) go(ps, k_gemm_bf16<64, 3>, dim3(grid), dim3(256), st, a);
     else go(ps, k_gemm_bf16<64, 4>, dim3(grid), dim3(256), st, a);

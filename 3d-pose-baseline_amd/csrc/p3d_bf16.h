@@ -171,6 +171,142 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmBf16Args p) {
   }
 }
 
+// Software-pipelined form of k_gemm_bf16 (same tiles, LDS ring and epilogue): the ds_reads
+// of k-group g+1 are issued before the MFMAs of group g (two fragment register sets), and
+// the first group of stage s+1 is read right after the one barrier per stage, so LDS
+// latency hides behind MFMA work at one wave per SIMD (the k_gemm_bf16 schedule waited
+// lgkmcnt(0) in front of every four MFMAs).  One barrier per stage: each wave drains its own
+// reads of stage s (lgkmcnt) before it, and the DMA refilling stage s's buffer is issued
+// after it.
+template <int BK, int NST, int WAVES, bool PRIO = false>
+__global__ __launch_bounds__(64 * WAVES) void k_gemm_bf16p(GemmBf16Args p) {
+  constexpr int KG = BK / 32;
+  constexpr int STAGE = (8 + 8) * KG * 1024;
+  constexpr int EPI = 128 * 132 * 4;
+  constexpr int LDS = (NST * STAGE > EPI) ? NST * STAGE : EPI;
+  constexpr int PER = 16 * KG / WAVES;            // LDS-DMA instructions per wave per stage
+  constexpr int CT = WAVES == 4 ? 4 : 2;          // 16-column MFMA tiles per wave (rows: 4)
+  constexpr int WN = 8 / CT;                      // waves along N
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tiles_n = p.N / 128, tiles_m = p.M / 128;
+  const int GM = (tiles_m % 4 == 0) ? 4 : ((tiles_m % 2 == 0) ? 2 : 1);
+  const int grp = tile_id / (GM * tiles_n), in_grp = tile_id % (GM * tiles_n);
+  const int mt = grp * GM + (in_grp % GM), nt = in_grp / GM;
+  const int ngA = p.K / 32;
+  const int nks = p.K / BK;
+  const unsigned char* Ag = (const unsigned char*)p.A + (int64_t)(8 * mt) * ngA * 1024;
+  const unsigned char* Bg = (const unsigned char*)p.Bt + (int64_t)(8 * nt) * ngA * 1024;
+
+  auto issue = [&](int ks, int buf) {
+    unsigned char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int t = w * PER + c;
+      const bool isB = t >= 8 * KG;
+      const int tt = isB ? t - 8 * KG : t;
+      const int j = tt / KG, g = tt % KG;
+      const unsigned char* src = (isB ? Bg : Ag) + ((int64_t)j * ngA + ks * KG + g) * 1024 + lane * 16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + t * 1024), 16, 0, 0);
+    }
+  };
+  auto read = [&](int buf, int g, bf16x8 (&af)[4], bf16x8 (&bfr)[CT]) {
+    const unsigned char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) af[r] = *(const bf16x8*)(base + ((4 * wm + r) * KG + g) * 1024 + lane * 16);
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+      bfr[c] = *(const bf16x8*)(base + (8 * KG + (CT * wn + c) * KG + g) * 1024 + lane * 16);
+  };
+
+  f32x4 acc[4][CT];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < CT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][4], fb[2][CT];
+
+#pragma unroll
+  for (int s0 = 0; s0 < NST - 1; ++s0)
+    if (s0 < nks) issue(s0, s0);
+  {
+    const int later = (nks - 1) < (NST - 2) ? (nks - 1) : (NST - 2);
+    p3d_wait_stages<PER, NST>(later);
+    __builtin_amdgcn_s_barrier();
+    read(0, 0, fa[0], fb[0]);
+  }
+  int cur = 0;
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks % NST;
+    if (ks + NST - 1 < nks) issue(ks + NST - 1, (ks + NST - 1) % NST);
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int nxt = cur ^ 1;
+      if (g + 1 < KG) {
+        read(buf, g + 1, fa[nxt], fb[nxt]);
+      } else if (ks + 1 < nks) {
+        // stage ks+1 must have landed (counted DMA wait) and every wave must be done
+        // reading stage ks before anyone refills it: drain this wave's reads, barrier,
+        // then prefetch the first group of stage ks+1
+        const int later = (nks - 2 - ks) < (NST - 2) ? (nks - 2 - ks) : (NST - 2);
+        p3d_wait_stages<PER, NST>(later);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        read((ks + 1) % NST, 0, fa[nxt], fb[nxt]);
+      }
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][r], fb[cur][c], acc[r][c], 0, 0, 0);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
+      cur = nxt;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // ---- epilogue (as k_gemm_bf16) ----
+  float* et = (float*)smem;
+  const int i = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        et[(64 * wm + 16 * r + 4 * q + e) * 132 + 16 * CT * wn + 16 * c + i] = acc[r][c][e];
+  __syncthreads();
+  const int ngY = p.N / 32;
+#pragma unroll
+  for (int it = 0; it < 2048 / (64 * WAVES); ++it) {
+    const int item = it * 64 * WAVES + tid;
+    const int chunk = item >> 6, l = item & 63;
+    const int rl = 16 * (chunk >> 2) + (l & 15);
+    const int cl = 32 * (chunk & 3) + 8 * (l >> 4);
+    const int row = 128 * mt + rl, col = 128 * nt + cl;
+    const int64_t off = p3d_pk16(row, col, ngY);
+    u16x8 rv;
+    if (p.res) rv = *(const u16x8*)(p.res + off);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int n = col + e;
+      float z = et[rl * 132 + cl + e] + p.epi.bias[n];
+      float y = p.epi.inv ? z * p.epi.inv[n] + p.epi.shift[n] : z;
+      if (p.epi.relu) y = fmaxf(y, 0.0f);
+      if (p.res) y += p3d_bf2f(rv[e]);
+      o[e] = p3d_f2bf(y);
+    }
+    *(u16x8*)(p.Y + off) = o;
+  }
+}
+
 // =====================================================================================
 // Small-N bf16 layer (output layer, N = 48): register-direct packed operands, 16 waves
 // split K (as k_fwd's inference tiling), fp32 row-major output.

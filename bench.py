@@ -458,8 +458,8 @@ def bench_stress(args, rank, world):
     flop = 2.0 * Bs * Ls * Ls
     achieved = flop / (avg_us * 1e-6) / 1e12
     roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16<64, 4>"),
-            "kernel": "k_gemm_bf16<64, 4> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16p<64, 4, 8, false>"),
+            "kernel": "k_gemm_bf16p<64, 4, 8, false> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps}
     model.close()
     return value, dt, roof, steps
