@@ -241,23 +241,17 @@ def bench_infer(args, rank, world):
         dt1 = timed(capture(1), args.steps)
         single = {"value": round(world * args.steps * BATCH / dt1, 1), "ms_per_step": round(1000.0 * dt1 / args.steps, 5)}
 
-    # dominant kernel, timed live: 200 launches of the first hidden layer (k_fwd<...,1>) on
-    # the model's stream, each carrying a start/stop event pair attached to its dispatch
-    # (hipExtLaunchKernel) -> average kernel duration, the interval rocprofv3 reports.
-    # b2b_avg_us: the same launches back to back under one event pair (adds the ~1 us
-    # dispatch gap between dependent kernels).
+    # dominant kernel, timed live: every hidden-layer launch (k_fwd<...,1>) of 100 steps
+    # issued on the model's stream in step order (the layers rotate through their weights as
+    # in the timed region), each carrying a start/stop event pair attached to its dispatch
+    # (hipExtLaunchKernel: the packet's own begin/end timestamps, the interval rocprofv3
+    # reports).  isolated_avg_us: one layer relaunched 200x with its weights hot, for reference.
     import _p3d
-    reps = 200
+    prof = profile_kernels(model, lambda: steps_eager(min(args.steps, 100)))
+    cnt, avg_us = prof["fwd_hidden"][0], prof["fwd_hidden"][1]
     lay = lambda n: _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, BATCH, n, model.stream()), "p3d_time_layer")
     lay(20)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    lay(reps)
-    e1.record()
-    torch.cuda.synchronize()
-    b2b_us = 1000.0 * e0.elapsed_time(e1) / reps
-    avg_us = profile_kernels(model, lambda: lay(reps))["fwd_hidden"][1]
-    prof = profile_kernels(model, lambda: steps_eager(min(args.steps, 100)))
+    iso_us = profile_kernels(model, lambda: lay(200))["fwd_hidden"][1]
     flop = 2.0 * BATCH * L * L          # one hidden-layer launch: [64,1024] x [1024,1024]
     achieved = flop / (avg_us * 1e-6) / 1e12
     kname = kernel_name(model, 0)
@@ -265,8 +259,9 @@ def bench_infer(args, rank, world):
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "kernel": kname + " (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
-            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
-            "b2b_avg_us": round(b2b_us, 3), "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": cnt,
+            "isolated_avg_us": round(iso_us, 3),
+            "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
     model.close()
     return value, dt, roof, single
 
@@ -387,20 +382,27 @@ def bench_eval(args, rank, world):
     frames = sum(nb) * BATCH
     assert int(round(t[:, 17].sum())) == frames, (t[:, 17].sum(), frames)
     errs = t[:, :17].sum(1) / (t[:, 17] * 17)
-    # dominant kernel of the sweep: a hidden layer at M = chunk rows (k_gemm_f32 when
-    # chunk >= 256), timed live with dispatch-attached events
-    import _p3d
-    lay = lambda n: _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, chunk, n, model.stream()), "p3d_time_layer")
-    lay(5)
-    prof = profile_kernels(model, lambda: lay(50))
-    tag = "fwd_hidden_big" if "fwd_hidden_big" in prof else "fwd_hidden"
-    avg_us = prof[tag][1]
-    flop = 2.0 * chunk * L * L
-    roof = {"bound": "mfma", "achieved": round(flop / (avg_us * 1e-6) / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(flop / (avg_us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "kernel": kernel_name(model, 1 if tag == "fwd_hidden_big" else 0) + " (hidden layer, M = %d)" % chunk,
-            "traffic": _committed_traffic(kernel_name(model, 1 if tag == "fwd_hidden_big" else 0)),
-            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3)}
+    # dominant kernel of the sweep: the large-M hidden layers (k_gemm_f32) of one whole
+    # sweep, each launch timed with dispatch-attached events; FLOPs from the chunk sizes
+    big_m = int(os.environ.get("P3D_BIG_M", "256"))
+    prof = profile_kernels(model, sweep)
+    big_rows = 0
+    for r in rows:
+        for s0 in range(0, r, chunk):
+            n = min(chunk, r - s0)
+            big_rows += n if n >= big_m else 0
+    tag = "fwd_hidden_big"
+    if tag in prof and big_rows:
+        cnt, avg_us = prof[tag][0], prof[tag][1]
+        flop = 2.0 * 2 * NBLK * big_rows * L * L        # 2N hidden layers per chunk
+        ach = flop / (cnt * avg_us * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_PEAK_TFLOPS, 4),
+                "kernel": kernel_name(model, 1) + " (hidden layers, %d-row launches)" % chunk,
+                "traffic": _committed_traffic(kernel_name(model, 1)),
+                "flop_per_launch": int(flop / cnt), "avg_us": round(avg_us, 3), "launches_timed": cnt}
+    else:
+        roof = None
     model.close()
     return {"workload": "cfg4 evaluateActionWise sweep: 15 actions, %d frames (tail-dropped), %s, "
                         "%d-row launches, sharded over %d rank(s)"
@@ -451,16 +453,20 @@ def bench_stress(args, rank, world):
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
     value = world * steps * Bs / dt
-    reps = 50
+    # hidden-layer launches of 8 steps in step order (32 MB of bf16 weights per layer,
+    # rotating), dispatch-attached events; isolated: one layer relaunched with hot weights
+    prof = profile_kernels(model, lambda: run(G))
+    reps, avg_us = prof["bf16_hidden"][0], prof["bf16_hidden"][1]
     lay = lambda n: _p3d.check(_p3d.lib().p3d_time_layer(model._h, 1, Bs, n, model.stream()), "p3d_time_layer")
     lay(5)
-    avg_us = profile_kernels(model, lambda: lay(reps))["bf16_hidden"][1]
+    iso_us = profile_kernels(model, lambda: lay(50))["bf16_hidden"][1]
     flop = 2.0 * Bs * Ls * Ls
     achieved = flop / (avg_us * 1e-6) / 1e12
     roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16p<64, 4, 8, false>"),
             "kernel": "k_gemm_bf16p<64, 4, 8, false> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
-            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps}
+            "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
+            "isolated_avg_us": round(iso_us, 3)}
     model.close()
     return value, dt, roof, steps
 
