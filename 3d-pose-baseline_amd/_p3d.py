@@ -66,6 +66,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise P3DError("libp3d.so not found at %s: the HIP extension is not built "
                        "(run __graft_entry__.build()); there is no CPU fallback" % path)
+    # One HIP runtime per process: torch's libc10_hip pulls in its bundled libamdhip64 by the
+    # unversioned name, libp3d.so by soname libamdhip64.so.7.  Loaded after torch, libp3d binds
+    # to torch's copy (same soname); loaded first, it would bring /opt/rocm's and torch would
+    # then add a second runtime, which sees no device (p3d_create: "no ROCm-capable device").
+    import torch  # noqa: F401
     lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

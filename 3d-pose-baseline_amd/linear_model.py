@@ -201,6 +201,7 @@ class LinearModel(object):
         self.world = dist.get_world_size() if self.data_parallel else 1
 
         self._loss_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._step_host = 0   # host mirror of the device global_step (step() summaries, no sync)
         self._dy = torch.empty((self.max_batch, self.output_size), dtype=torch.float32, device=self.device)
         if init:
             self.initialize(self.seed)
@@ -294,6 +295,7 @@ class LinearModel(object):
         self.flat["adam_m"].zero_()
         self.flat["adam_v"].zero_()
         check(lib().p3d_set_step(self._h, 0, 0.9, 0.999), "p3d_set_step")
+        self._step_host = 0
         if self.data_parallel:
             self.broadcast_parameters()
 
@@ -342,6 +344,7 @@ class LinearModel(object):
         if "global_step" in st:
             check(lib().p3d_set_step(self._h, int(st["global_step"]), float(st["beta1_power"]),
                                      float(st["beta2_power"])), "p3d_set_step")
+            self._step_host = int(st["global_step"])
 
     def broadcast_parameters(self):
         """Rank 0's variables to every rank (start of data-parallel training)."""
@@ -405,6 +408,7 @@ class LinearModel(object):
         if self.data_parallel:
             self._allreduce_grads()
         check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
+        self._step_host += 1
         return loss, y
 
     def compute_gradients(self, x, t, keep_prob, ctr=None):
@@ -435,7 +439,7 @@ class LinearModel(object):
         torch = self.torch
         with torch.cuda.device(self.device):
             if isTraining:
-                lr = exponential_decay(self.lr0, self.get_step()[0])
+                lr = exponential_decay(self.lr0, self._step_host)   # lr of this step (gs before the update)
                 loss, y = self.train_step_device(encoder_inputs, decoder_outputs, dropout_keep_prob)
                 out = y.cpu().numpy()
                 lv = float(loss.item())

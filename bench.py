@@ -411,6 +411,31 @@ def bench_eval(args, rank, world):
             "average_mm": round(float(np.mean(errs)), 6), "roofline": roof}
 
 
+def bench_api(args, rank, world, n_infer=300, n_train=100):
+    """API-level rates: LinearModel.step() fed numpy batches of 64 exactly as the
+    reference's session.run path is (float64 host arrays -> H2D, outputs D2H, loss to host
+    every step), eval and train.  Includes every host round trip; the device-resident rates
+    are the headline and "train"."""
+    import torch
+    model, _ = make_model(data_parallel=world > 1)
+    rng = np.random.default_rng(500 + rank)
+    xs = [rng.standard_normal((BATCH, IN)) for _ in range(8)]
+    ts = [rng.standard_normal((BATCH, OUT)) for _ in range(8)]
+    out = {}
+    for name, n, train, keep in (("eval", n_infer, False, 1.0), ("train", n_train, True, 0.5)):
+        for i in range(10):
+            model.step(None, xs[i % 8], ts[i % 8], keep, isTraining=train)
+        barrier_sync(world)
+        t0 = time.perf_counter()
+        for i in range(n):
+            model.step(None, xs[i % 8], ts[i % 8], keep, isTraining=train)
+        barrier_sync(world)
+        dt = max_over_ranks(time.perf_counter() - t0, world)
+        out[name] = {"value": round(world * n * BATCH / dt, 1), "unit": "poses/s", "ms_per_step": round(1000.0 * dt / n, 4)}
+    model.close()
+    return out
+
+
 def bench_stress(args, rank, world):
     """cfg5: L=4096, 4 residual blocks, bf16 weights/activations with fp32 accumulate and
     fp32 BN, batch 1024, inference.  One step = one forward of one batch of 1024 poses."""
@@ -487,6 +512,7 @@ def main():
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
+    ap.add_argument("--no-api", action="store_true", help="skip the LinearModel.step() API-level rates (infer mode)")
     ap.add_argument("--procrustes", action="store_true", help="cfg4 sweep with Protocol #2 alignment")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
@@ -494,7 +520,7 @@ def main():
     rank, world, local = setup_dist()
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    train = single = sweep = None
+    train = single = sweep = api = None
     if args.mode == "infer":
         value, dt, roof, single = bench_infer(args, rank, world)
         workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
@@ -513,6 +539,11 @@ def main():
                 sweep = bench_eval(args, rank, world)
             except Exception as exc:
                 sweep = {"error": repr(exc)[:300]}
+        if not args.no_api:
+            try:
+                api = bench_api(args, rank, world)
+            except Exception as exc:
+                api = {"error": repr(exc)[:300]}
     elif args.mode == "eval":
         sweep = bench_eval(args, rank, world)
         value, dt, roof = sweep["value"], sweep["ms_per_sweep"] / 1000.0, sweep.pop("roofline")
@@ -548,6 +579,8 @@ def main():
             line["train"] = train
         if sweep is not None and args.mode != "eval":
             line["eval_sweep"] = sweep
+        if api is not None:
+            line["api_step"] = api
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
