@@ -56,6 +56,8 @@ SIGNATURES = [
     ("p3d_mpjpe_accum_ex", c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_kernel_name", c_int32, [c_void_p, c_int32, c_char_p, c_int64]),
+    ("p3d_train_fwd_bwd", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
+                                    c_void_p, c_void_p]),
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),
     ("p3d_profile_stop", c_int32, [c_void_p, c_char_p, c_int64]),
     ("p3d_time_layer", c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p]),

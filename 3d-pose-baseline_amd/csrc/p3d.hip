@@ -49,6 +49,10 @@ struct FwdArgs {
   const float* res;               // residual added after dropout, packed [M, N]
   float* Y; int64_t ldy;          // packed (hidden) or row-major (output layer)
   float* bnpart;                  // bn == 3: per (row tile, column) {sum z, sum (z - tile mean)^2}
+  const float* tgt;               // fused MSE (training output layer, row-major like Y): targets,
+  float* dy; float dscale;        //   dy = dscale * (y - t) stored row-major (leading dim lddy),
+  int64_t lddy;
+  float* lossp;                   //   per-workgroup sum of (y - t)^2
 };
 
 // Phase timestamps for kernel development (build with -DP3D_TRACE; tools/trace_train.py).
@@ -184,6 +188,24 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu[s]);
   }
   if (trace) P3D_STAMP(4);
+  if (p.tgt) {
+    // fused MSE of linear_model.py:129 (output layer: no BN / ReLU / dropout / residual)
+    float ls = 0.f;
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 16 * s + 4 * q + r;
+        if (cok && row < p.M) {
+          const float d = z[s][r] - p.tgt[(int64_t)row * p.ldy + col];
+          p.dy[(int64_t)row * p.lddy + col] = d * p.dscale;
+          ls += d * d;
+        }
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+    if (lane == 0) p.lossp[blockIdx.x + gridDim.x * blockIdx.y] = ls;
+  }
   if (!cok) return;
 #pragma unroll
   for (int s = 0; s < RS; ++s)
@@ -325,6 +347,8 @@ struct BwdArgs {
   float* dgamma; float* dbeta;    // [K]
   float* bnpart;                  // split BN backward: per (row tile, column) {sum g, sum g*xhat};
                                   // dz then holds g (k_bn_bwd finishes it)
+  const float* lossp; int nlossp; // fused MSE: workgroup 0 folds the forward's loss partials
+  float* loss; float loss_scale;  //   (fixed order) into loss[0] = scale * sum
 };
 
 // RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
@@ -339,6 +363,11 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   const bool cok = col < p.K;
   const int cc = cok ? col : p.K - 1;
   const int ngK = p.K >> 4;
+  if (p.lossp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    float l = 0.f;
+    for (int k = 0; k < p.nlossp; ++k) l += p.lossp[k];
+    p.loss[0] = l * p.loss_scale;
+  }
   // prefetch the epilogue's per-column and per-element operands
   float mean = 0.f, var = 1.f, gam = 1.f, bet = 0.f, zz[RS][4], dr[RS][4];
   uint64_t ctr = p.ctr;
@@ -909,6 +938,10 @@ struct p3d_model {
   float* ws = nullptr;        // activation workspace
   float* scratch = nullptr;   // reductions (max-norm)
   float* bnpart = nullptr;    // inside scratch: split BN-train row-tile partials
+  float* lossp = nullptr;     // inside scratch: fused-MSE per-workgroup loss partials (<= 64)
+  int nlossp = 0;
+  float* loss_dst = nullptr;  // set during p3d_train_fwd_bwd: the backward folds the loss here
+  float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
@@ -1146,8 +1179,10 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   m->dout[0] = cur; cur += pad64(Bp * L);
   m->dout[1] = cur; cur += pad64(Bp * L);
-  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + 4 * 2 * (int64_t)L;
+  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + 4 * 2 * (int64_t)L + 64 +
+                            pad64((int64_t)c.max_batch * c.output_size);
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->scratch, 0, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev);
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
@@ -1164,6 +1199,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
   m->gw = m->wsq + 64;
   m->bnpart = m->gw + 64;   // [4 row tiles][L][2]: split BN-train partial moments / sums
+  m->lossp = m->bnpart + 4 * 2 * (int64_t)L;
+  m->dybuf = m->lossp + 64;
   // TF defaults: BN gamma = 1, moving_variance = 1 (beta/mean = 0 already)
   if (c.batch_norm) {
     std::vector<float> ones(L, 1.0f);
@@ -1460,9 +1497,21 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
   return P3D_OK;
 }
 
+static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32_t training, float keep_prob,
+                        uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row, void* stream,
+                        const float* tgt);
+
 extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t training,
                               float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row,
                               void* stream) {
+  return forward_impl(m, x, B, y, training, keep_prob, seed, ctr, row_offset, ws_row, stream, nullptr);
+}
+
+// tgt != null (training): the output layer also forms dy = 2(y - t)/(B*D) into m->dybuf and
+// per-workgroup loss partials into m->lossp (p3d_train_fwd_bwd).
+static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32_t training, float keep_prob,
+                        uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row, void* stream,
+                        const float* tgt) {
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_forward: null argument");
   const p3d_cfg& c = m->cfg;
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_forward: batch must be positive");
@@ -1512,6 +1561,11 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
     if (c.residual && second) a.res = m->act[l - 2] + wsoff;
     if (last) { a.Y = y; a.ldy = ly.N; }
     else { a.Y = m->act[l] + wsoff; a.ldy = 0; }
+    if (last && tgt) {
+      a.tgt = tgt; a.dy = m->dybuf; a.lddy = (ly.N + 15) / 16 * 16;
+      a.dscale = (1.0f / (float)(B * ly.N)) * 2.0f; a.lossp = m->lossp;
+      m->nlossp = (int)(((ly.N + 15) / 16) * ((B + 15) / 16));
+    }
     const int kind = (l == 0) ? 0 : (last ? 2 : 1);
     if (training && ly.bn && m->train_split) {
       const int rc = launch_fwd_split(m, a, kind, st);
@@ -1596,9 +1650,19 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (B != m->B_cached) return fail(P3D_ERR_ARG, "p3d_backward: batch differs from the training forward");
   if (B > 64) return fail(P3D_ERR_ARG, "p3d_backward: B <= 64 in this build");
   const p3d_cfg& c = m->cfg;
-  if (c.output_size % 16 != 0 || !aligned16(dy))
-    return fail(P3D_ERR_ARG, "p3d_backward: output_size must be a multiple of 16 and dy 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
+  // dy enters the output layer's GEMMs as a row-major operand read in 16-column groups:
+  // use it in place when its rows are 16-float aligned, else through the zero-padded dybuf
+  const int np_out = (c.output_size + 15) / 16 * 16;
+  int64_t ld_dy = c.output_size;
+  if (dy == m->dybuf) {
+    ld_dy = np_out;
+  } else if (c.output_size % 16 != 0 || !aligned16(dy)) {
+    HIP_TRY(hipMemcpy2DAsync(m->dybuf, (size_t)np_out * 4, dy, (size_t)c.output_size * 4,
+                             (size_t)c.output_size * 4, (size_t)B, hipMemcpyDeviceToDevice, st));
+    dy = m->dybuf;
+    ld_dy = np_out;
+  }
   const int nl = (int)m->layers.size();
   float* grads = m->flat[1];
   const float* params = m->flat[0];
@@ -1610,7 +1674,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     const Layer& ly = m->layers[l];
     WgradArgs wa{};
     wa.X = (l == 0) ? m->x_cached : m->act[l - 1]; wa.ldx = c.input_size; wa.xpk = (l != 0);
-    wa.dZ = dz_cur; wa.ldz = ly.N; wa.zpk = dz_pk;
+    wa.dZ = dz_cur; wa.ldz = dz_pk ? ly.N : ld_dy; wa.zpk = dz_pk;
     wa.M = (int)B; wa.K = ly.K; wa.N = ly.N;
     wa.dW = grads + ly.w; wa.db = grads + ly.b;
     int rc = launch_wgrad(m, wa, st);
@@ -1618,7 +1682,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     if (l == 0) break;
     const Layer& pv = m->layers[l - 1];
     BwdArgs a{};
-    a.dZ = dz_cur; a.ldz = ly.N;
+    a.dZ = dz_cur; a.ldz = dz_pk ? ly.N : ld_dy;
     a.Wd = m->wpk + ly.wd; a.ngB = (ly.N + 15) / 16;
     a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
     a.M = (int)B; a.K = ly.K; a.N = ly.N;
@@ -1631,6 +1695,10 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         a.dres = dres_next;                  // dX of a block input = dZ*W^T + d(block output)
         if (l - 1 >= 1) a.draw = m->dout[dsel];
       }
+    }
+    if (is_out && m->loss_dst) {
+      a.lossp = m->lossp; a.nlossp = m->nlossp; a.loss = m->loss_dst;
+      a.loss_scale = 1.0f / (float)(B * ly.N);
     }
     a.prev = 1;
     a.bn = pv.bn;
@@ -1688,6 +1756,25 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     LAUNCH_CHECK("k_maxnorm_grad");
   }
   return P3D_OK;
+}
+
+// Forward (training, dropout counter from the device step state) + fused MSE + backward,
+// one call: the loss lands in loss_dev, the gradients in the flat grads buffer.  The
+// output layer forms dy and the loss partials in its epilogue; the first backward kernel
+// folds the partials (no k_mse launch).
+extern "C" int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
+                                 float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,
+                                 void* stream) {
+  if (!m || !x || !t || !y || !loss_dev) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: null argument");
+  if (m->cfg.dtype != P3D_DTYPE_F32) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: bf16 models are inference-only");
+  if (B <= 0 || B > 64) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: B must be in 1..64");
+  if (!aligned16(t)) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: t must be 16-byte aligned");
+  int rc = forward_impl(m, x, B, y, 1, keep_prob, seed, P3D_CTR_GLOBAL_STEP, row_offset, 0, stream, t);
+  if (rc) return rc;
+  m->loss_dst = loss_dev;
+  rc = p3d_backward(m, m->dybuf, B, stream);
+  m->loss_dst = nullptr;
+  return rc;
 }
 
 static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st) {

@@ -399,12 +399,15 @@ class LinearModel(object):
         if B > self.max_batch:
             raise ValueError("batch %d exceeds max_batch %d" % (B, self.max_batch))
         self._x_keep = x  # the library differentiates this buffer in p3d_backward
-        # dropout counter, lr decay and the Adam beta powers all come from the device-side
-        # step state, so this sequence is capturable in a HIP graph
-        y = self.forward_device(x, True, keep_prob, out=out, ctr=_p3d.P3D_CTR_GLOBAL_STEP)
-        dy = self._dy[:B]
-        loss = self.loss_device(y, t, dy)
-        check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
+        if out is None:
+            out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
+        y = out
+        # forward + fused MSE + backward in one call; the dropout counter, lr decay and the
+        # Adam beta powers all come from the device-side step state, so this sequence is
+        # capturable in a HIP graph
+        check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
+                                      self.rank * B, ptr(self._loss_dev), self.stream()), "p3d_train_fwd_bwd")
+        loss = self._loss_dev
         if self.data_parallel:
             self._allreduce_grads()
         check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")

@@ -113,6 +113,14 @@ int p3d_mse(const float* y, const float* t, int64_t B, int32_t D, float* loss_de
  * into the flat grads buffer (opt.compute_gradients, linear_model.py:143). */
 int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stream);
 
+/* p3d_forward(training = 1, ctr = P3D_CTR_GLOBAL_STEP) + p3d_mse + p3d_backward in one
+ * call (session.run of the train op up to compute_gradients, linear_model.py:129,143):
+ * x [B,32], t [B,48] device row-major, B <= 64; outputs y [B,48]; loss_dev = mean((y-t)^2);
+ * gradients in the flat grads buffer.  The MSE runs in the output layer's epilogue. */
+int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
+                      float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,
+                      void* stream);
+
 /* One TF1 ApplyAdam over all trainables (linear_model.py:137,145):
  *   alpha = lr*sqrt(1-beta2_power)/(1-beta1_power); m += (g-m)(1-b1);
  *   v += (g^2-v)(1-b2); w -= (m*alpha)/(sqrt(v)+eps)

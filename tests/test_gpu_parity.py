@@ -155,6 +155,38 @@ def test_train_steps_track_oracle(split, monkeypatch):
     m.close()
 
 
+def test_predict14_gradients_and_train_steps():
+    """--predict_14 (42 outputs, not a multiple of 16): backward through the zero-padded dy
+    path and the fused-MSE train step, vs the oracle."""
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=True, batch_norm=True, predict_14=True)
+    st, m = make(cfg, lr=1e-3)
+    assert m.output_size == 42
+    rng = np.random.default_rng(14)
+    x = rng.standard_normal((64, 32))
+    t = rng.standard_normal((64, 42))
+    loss, y = m.compute_gradients(x, t, 0.5, ctr=2)
+    out, cache = ref_mlp.forward(st, x, True, 0.5, m.seed, 2, 0)
+    rl, dy = ref_mlp.mse(out, t)
+    grads = ref_mlp.backward(st, cache, dy)
+    close(y.cpu().numpy(), out, atol=5e-5, rtol=5e-5)
+    for name in m.trainable_names():
+        if "/b1" in name or "/b2_" in name or "/b3_" in name:
+            continue
+        g = m.grad(name).cpu().numpy()
+        r = grads[name]
+        assert np.abs(g - r).max() / max(np.abs(r).max(), 1e-30) < 1e-3, name
+    m.close()
+    st, m = make(cfg, lr=1e-3)
+    for step in range(3):
+        x = rng.standard_normal((64, 32))
+        t = rng.standard_normal((64, 42))
+        loss, _, _, out = m.step(None, x, t, 0.5, isTraining=True)
+        rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
+        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=1e-3, rtol=1e-3)
+    m.close()
+
+
 def test_mpjpe_kernel_matches_reference_goldens():
     g = np.load("tests/golden/reference_goldens.npz", allow_pickle=False)
     st, m = make(ref_mlp.Cfg(linear_size=256, num_layers=1))
