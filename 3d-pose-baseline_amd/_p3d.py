@@ -56,6 +56,9 @@ SIGNATURES = [
     ("p3d_mpjpe_accum_ex", c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_kernel_name", c_int32, [c_void_p, c_int32, c_char_p, c_int64]),
+    ("p3d_dlpack_alias", c_void_p, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32]),
+    ("p3d_train_step", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_float,
+                                 c_float, c_float, c_void_p, c_void_p]),
     ("p3d_train_fwd_bwd", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
                                     c_void_p, c_void_p]),
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),
@@ -104,60 +107,21 @@ def check(rc: int, what: str = ""):
 # --------------------------------------------------------------------------------------
 
 
-class _DLDevice(ctypes.Structure):
-    _fields_ = [("device_type", c_int32), ("device_id", c_int32)]
-
-
-class _DLDataType(ctypes.Structure):
-    _fields_ = [("code", ctypes.c_uint8), ("bits", ctypes.c_uint8), ("lanes", ctypes.c_uint16)]
-
-
-class _DLTensor(ctypes.Structure):
-    _fields_ = [("data", c_void_p), ("device", _DLDevice), ("ndim", c_int32),
-                ("dtype", _DLDataType), ("shape", POINTER(c_int64)),
-                ("strides", POINTER(c_int64)), ("byte_offset", c_uint64)]
-
-
-class _DLManagedTensor(ctypes.Structure):
-    pass
-
-
-_DELETER = ctypes.CFUNCTYPE(None, POINTER(_DLManagedTensor))
-_DLManagedTensor._fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", c_void_p),
-                             ("deleter", _DELETER)]
-
-_KEEPALIVE = {}
-_kDLROCM = 10
-
-
-@_DELETER
-def _noop_deleter(ptr):  # memory is owned by the p3d model handle
-    _KEEPALIVE.pop(ctypes.addressof(ptr.contents), None)
-
-
 def device_view(ptr: int, shape, device_index: int, dtype_code: int = 2, bits: int = 32):
-    """torch tensor aliasing ``ptr`` (no copy).  The owner must outlive the view."""
-    import torch
+    """torch tensor aliasing ``ptr`` (no copy).  The owner must outlive the view.  The
+    DLPack record and its deleter are native (p3d_dlpack_alias): releasing the view never
+    re-enters Python, also not during interpreter teardown."""
     from torch.utils.dlpack import from_dlpack
 
     shape = tuple(int(s) for s in shape)
     shp = (c_int64 * len(shape))(*shape)
-    mt = _DLManagedTensor()
-    mt.dl_tensor.data = ptr
-    mt.dl_tensor.device = _DLDevice(_kDLROCM, device_index)
-    mt.dl_tensor.ndim = len(shape)
-    mt.dl_tensor.dtype = _DLDataType(dtype_code, bits, 1)
-    mt.dl_tensor.shape = shp
-    mt.dl_tensor.strides = None
-    mt.dl_tensor.byte_offset = 0
-    mt.manager_ctx = None
-    mt.deleter = _noop_deleter
-    _KEEPALIVE[ctypes.addressof(mt)] = (mt, shp)
+    mt = lib().p3d_dlpack_alias(c_void_p(ptr), len(shape), shp, int(device_index), int(dtype_code), int(bits))
+    if not mt:
+        raise P3DError("p3d_dlpack_alias failed")
     PyCapsule_New = ctypes.pythonapi.PyCapsule_New
     PyCapsule_New.restype = ctypes.py_object
     PyCapsule_New.argtypes = [c_void_p, c_char_p, c_void_p]
-    cap = PyCapsule_New(ctypes.addressof(mt), b"dltensor", None)
-    t = from_dlpack(cap)
+    t = from_dlpack(PyCapsule_New(mt, b"dltensor", None))
     assert t.data_ptr() == ptr
     return t
 

@@ -29,6 +29,110 @@
 #include <vector>
 
 // =====================================================================================
+// TF1 ApplyAdam primitives (linear_model.py:137,145) shared by k_adam_pack and the fused
+// single-GPU train step (k_wgrad / k_bn_bwd apply the update where the gradient is formed)
+// =====================================================================================
+#define P3D_MAX_W 40
+#define P3D_MAX_V 64
+struct StepState {
+  int64_t global_step;
+  float beta1_power, beta2_power;
+  unsigned int arrivals;
+  unsigned int pad[3];
+};
+
+// Every operation rounded on its own (no FMA contraction), as the TF1 kernel's expression
+// reads and as the oracle computes it -- and identically in every kernel that inlines it
+// (the compiler contracted it in one context and not in another before).
+__device__ __forceinline__ void p3d_adam1(float& w, float& m, float& v, float g, float alpha, float omb1,
+                                          float omb2, float eps) {
+#pragma clang fp contract(off)
+  m = m + (g - m) * omb1;
+  v = v + (g * g - v) * omb2;
+  w = w - (m * alpha) / (sqrtf(v) + eps);
+}
+
+// Adam hyper-parameters + the device step state a fused kernel reads its alpha from.
+struct AdamFuse {
+  const StepState* st;
+  float lr_host;        // >= 0: use as lr; < 0: device exponential decay of lr0
+  float lr0, decay_steps, decay_rate;
+  float b1, b2, eps;
+};
+
+__device__ __forceinline__ float p3d_adam_alpha(const StepState* st, float lr_host, float lr0, float decay_steps,
+                                                float decay_rate) {
+  const float b1p = st->beta1_power, b2p = st->beta2_power;
+  float lr = lr_host;
+  if (lr < 0.f) lr = lr0 * powf(decay_rate, (float)st->global_step / decay_steps);
+  return lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+}
+
+// Adam on one 64x64 tile (rows k0.., cols n0..) of a weight W [K, N] (TF layout, flat
+// offset `off` in w/m/v/g) + re-pack of the updated tile into Wf / Wd.  256 threads.
+// g comes from `g` (global) or, when g == nullptr, from tile[k - k0][n - n0] (the fused
+// weight-gradient kernel); tile ends holding the updated weights.  Bit-identical updates
+// either way (same gradient values, same p3d_adam1).
+__device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* g, int64_t off, int K, int N,
+                                                int k0, int n0, float* w, float* m, float* v, float* wd,
+                                                float* wf, float alpha, float omb1, float omb2, float eps) {
+  const int tid = threadIdx.x;
+  const bool vec = (N & 3) == 0;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+    const int k = k0 + r, n = n0 + c;
+    float wn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (k < K) {
+      const int64_t base = off + (int64_t)k * N + n;
+      if (vec && n + 3 < N) {
+        f32x4 ww = *(f32x4*)(w + base), mm = *(f32x4*)(m + base), vv = *(f32x4*)(v + base);
+        f32x4 gg;
+        if (g) gg = *(const f32x4*)(g + base);
+        else gg = f32x4{tile[r][c], tile[r][c + 1], tile[r][c + 2], tile[r][c + 3]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float w1 = ww[e], m1 = mm[e], v1 = vv[e];
+          p3d_adam1(w1, m1, v1, gg[e], alpha, omb1, omb2, eps);
+          ww[e] = w1; mm[e] = m1; vv[e] = v1; wn[e] = w1;
+        }
+        *(f32x4*)(w + base) = ww; *(f32x4*)(m + base) = mm; *(f32x4*)(v + base) = vv;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < N) {
+            float ww = w[base + e], mm = m[base + e], vv = v[base + e];
+            p3d_adam1(ww, mm, vv, g ? g[base + e] : tile[r][c + e], alpha, omb1, omb2, eps);
+            w[base + e] = ww; m[base + e] = mm; v[base + e] = vv;
+            wn[e] = ww;
+          }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];   // each thread rewrites only what it read
+  }
+  __syncthreads();
+  const int NP = (N + 15) & ~15;
+  const int ngf = K >> 4, ngd = NP >> 4;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int sub = it * 4 + (tid >> 6), l = tid & 63;
+    const int sk = sub >> 2, sn = sub & 3;             // 16x16 sub-tile within the 64x64 tile
+    const int kt = (k0 >> 4) + sk, nt = (n0 >> 4) + sn;
+    if (16 * kt >= K || 16 * nt >= NP) continue;
+    const int i = l & 15, q = l >> 4;
+    // Wd (rows k, cols n): element (16kt+i, 16nt+4q+e)
+    const f32x4 od = f32x4{tile[16 * sk + i][16 * sn + 4 * q], tile[16 * sk + i][16 * sn + 4 * q + 1],
+                           tile[16 * sk + i][16 * sn + 4 * q + 2], tile[16 * sk + i][16 * sn + 4 * q + 3]};
+    *(f32x4*)(wd + ((int64_t)(kt * ngd + nt) * 64 + l) * 4) = od;
+    // Wf (rows n, cols k): element (16nt+i, 16kt+4q+e)
+    const f32x4 of = f32x4{tile[16 * sk + 4 * q][16 * sn + i], tile[16 * sk + 4 * q + 1][16 * sn + i],
+                           tile[16 * sk + 4 * q + 2][16 * sn + i], tile[16 * sk + 4 * q + 3][16 * sn + i]};
+    *(f32x4*)(wf + ((int64_t)(nt * ngf + kt) * 64 + l) * 4) = of;
+  }
+}
+
+// =====================================================================================
 // forward
 // =====================================================================================
 struct FwdArgs {
@@ -528,6 +632,14 @@ struct WgradArgs {
   int M, K, N;
   float* dW;                      // [K, N] (TF layout, into the flat grads buffer)
   float* db;                      // [N] or null
+  // fused Adam (single-GPU train step): instead of storing dW / db, apply the update to
+  // W (flat offset woff) / b (boff) in w/m/v and re-pack the tile into Wf / Wd
+  int adam; AdamFuse af;
+  float* w; float* m; float* v; int64_t woff, boff;
+  float* wd; float* wf;
+  // ... and to the previous layer's BN gamma / beta ([K]; flat offsets goff / btoff), whose
+  // gradients k_bn_bwd wrote to gflat just before (all readers of gamma/beta are done)
+  int bn_adam; const float* gflat; int64_t goff, btoff;
 };
 
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
@@ -591,10 +703,45 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
     }
     __syncthreads();
   }
+  float alpha = 0.f;
+  if (p.adam) alpha = p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
   if (do_db) {
     dbp[w][lane] = dbs;
     __syncthreads();
-    if (w == 0 && n0 + lane < p.N) p.db[n0 + lane] = ((dbp[0][lane] + dbp[1][lane]) + dbp[2][lane]) + dbp[3][lane];
+    if (w == 0 && n0 + lane < p.N) {
+      const float gb = ((dbp[0][lane] + dbp[1][lane]) + dbp[2][lane]) + dbp[3][lane];
+      if (p.adam) {
+        p.db[n0 + lane] = gb;   // the bias gradient stays visible in the grads buffer
+        const int64_t o = p.boff + n0 + lane;
+        float ww = p.w[o], mm = p.m[o], vv = p.v[o];
+        p3d_adam1(ww, mm, vv, gb, alpha, 1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps);
+        p.w[o] = ww; p.m[o] = mm; p.v[o] = vv;
+      } else {
+        p.db[n0 + lane] = gb;
+      }
+    }
+  }
+  if (p.adam && p.bn_adam && blockIdx.x == 0 && tid < 64 && k0 + tid < p.K) {
+    const float omb1 = 1.0f - p.af.b1, omb2 = 1.0f - p.af.b2;
+    const int64_t og = p.goff + k0 + tid, ob = p.btoff + k0 + tid;
+    float w1 = p.w[og], m1 = p.m[og], v1 = p.v[og];
+    p3d_adam1(w1, m1, v1, p.gflat[og], alpha, omb1, omb2, p.af.eps);
+    p.w[og] = w1; p.m[og] = m1; p.v[og] = v1;
+    float w2 = p.w[ob], m2 = p.m[ob], v2 = p.v[ob];
+    p3d_adam1(w2, m2, v2, p.gflat[ob], alpha, omb1, omb2, p.af.eps);
+    p.w[ob] = w2; p.m[ob] = m2; p.v[ob] = v2;
+  }
+  if (p.adam) {
+    // gradient tile -> LDS (reusing the staging buffer), then Adam + re-pack of W's tile
+    float (*tile)[65] = reinterpret_cast<float (*)[65]>(xs);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tile[16 * w + 4 * q + r][16 * s + i] = acc[s][r];
+    __syncthreads();
+    p3d_adam_tile64(tile, nullptr, p.woff, p.K, p.N, k0, n0, p.w, p.m, p.v, p.wd, p.wf, alpha,
+                    1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps);
+    return;
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -618,15 +765,6 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
 // tile is also written in both fragment-major layouts (Wd directly, Wf via an LDS
 // transpose); 1-D tensors (biases, gamma, beta) are updated float-wise.
 // =====================================================================================
-#define P3D_MAX_W 40
-#define P3D_MAX_V 64
-struct StepState {
-  int64_t global_step;
-  float beta1_power, beta2_power;
-  unsigned int arrivals;
-  unsigned int pad[3];
-};
-
 struct AdamTable {
   int nw, nv;
   int K[P3D_MAX_W], N[P3D_MAX_W];
@@ -646,13 +784,6 @@ struct AdamArgs {
   float b1, b2, eps;
   int wblocks;          // blocks spent on weight tiles (one 64x64 tile each)
 };
-
-__device__ __forceinline__ void p3d_adam1(float& w, float& m, float& v, float g, float alpha, float omb1,
-                                          float omb2, float eps) {
-  m += (g - m) * omb1;
-  v += (g * g - v) * omb2;
-  w -= (m * alpha) / (sqrtf(v) + eps);
-}
 
 // One 64x64 weight tile per 256-thread block: 16 threads x float4 per 256-B row segment;
 // the updated tile is staged in LDS and written as 16 Wd and 16 Wf fragment-major 1 KB
@@ -677,58 +808,8 @@ __global__ __launch_bounds__(256) void k_adam_pack(AdamArgs a, AdamTable tb) {
     const int tnc = (N + 63) >> 6;
     const int local = tile_id - tb.tile_begin[wi];
     const int k0 = (local / tnc) * 64, n0 = (local % tnc) * 64;
-    const bool vec = (N & 3) == 0;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
-      const int k = k0 + r, n = n0 + c;
-      float wn[4] = {0.f, 0.f, 0.f, 0.f};
-      if (k < K) {
-        const int64_t base = tb.off[wi] + (int64_t)k * N + n;
-        if (vec && n + 3 < N) {
-          f32x4 ww = *(f32x4*)(a.w + base), mm = *(f32x4*)(a.m + base), vv = *(f32x4*)(a.v + base);
-          const f32x4 gg = *(const f32x4*)(a.g + base);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float w1 = ww[e], m1 = mm[e], v1 = vv[e];
-            p3d_adam1(w1, m1, v1, gg[e], alpha, omb1, omb2, a.eps);
-            ww[e] = w1; mm[e] = m1; vv[e] = v1; wn[e] = w1;
-          }
-          *(f32x4*)(a.w + base) = ww; *(f32x4*)(a.m + base) = mm; *(f32x4*)(a.v + base) = vv;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n + e < N) {
-              float ww = a.w[base + e], mm = a.m[base + e], vv = a.v[base + e];
-              p3d_adam1(ww, mm, vv, a.g[base + e], alpha, omb1, omb2, a.eps);
-              a.w[base + e] = ww; a.m[base + e] = mm; a.v[base + e] = vv;
-              wn[e] = ww;
-            }
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];
-    }
-    __syncthreads();
-    // 16 sub-tiles of 16x16; thread = (sub-tile group of 4 threads? no: lane of a chunk)
-    const int NP = (N + 15) & ~15;
-    const int ngf = K >> 4, ngd = NP >> 4;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int sub = it * 4 + (tid >> 6), l = tid & 63;
-      const int sk = sub >> 2, sn = sub & 3;             // 16x16 sub-tile within the 64x64 tile
-      const int kt = (k0 >> 4) + sk, nt = (n0 >> 4) + sn;
-      if (16 * kt >= K || 16 * nt >= NP) continue;
-      const int i = l & 15, q = l >> 4;
-      // Wd (rows k, cols n): element (16kt+i, 16nt+4q+e)
-      const f32x4 od = f32x4{tile[16 * sk + i][16 * sn + 4 * q], tile[16 * sk + i][16 * sn + 4 * q + 1],
-                             tile[16 * sk + i][16 * sn + 4 * q + 2], tile[16 * sk + i][16 * sn + 4 * q + 3]};
-      *(f32x4*)(a.wpk + tb.wd[wi] + ((int64_t)(kt * ngd + nt) * 64 + l) * 4) = od;
-      // Wf (rows n, cols k): element (16nt+i, 16kt+4q+e)
-      const f32x4 of = f32x4{tile[16 * sk + 4 * q][16 * sn + i], tile[16 * sk + 4 * q + 1][16 * sn + i],
-                             tile[16 * sk + 4 * q + 2][16 * sn + i], tile[16 * sk + 4 * q + 3][16 * sn + i]};
-      *(f32x4*)(a.wpk + tb.wf[wi] + ((int64_t)(nt * ngf + kt) * 64 + l) * 4) = of;
-    }
+    p3d_adam_tile64(tile, a.g, tb.off[wi], K, N, k0, n0, a.w, a.m, a.v, a.wpk + tb.wd[wi], a.wpk + tb.wf[wi],
+                    alpha, omb1, omb2, a.eps);
   } else {
     const int chunk = blockIdx.x - a.wblocks;
     if (chunk < tb.vbegin[tb.nv]) {
@@ -941,6 +1022,9 @@ struct p3d_model {
   float* lossp = nullptr;     // inside scratch: fused-MSE per-workgroup loss partials (<= 64)
   int nlossp = 0;
   float* loss_dst = nullptr;  // set during p3d_train_fwd_bwd: the backward folds the loss here
+  const AdamFuse* fuse_adam = nullptr;  // set during p3d_train_step: Adam fused into the backward
+  int adam_in_wgrad = 0;      // env P3D_FUSE_ADAM=1: p3d_train_step applies Adam inside k_wgrad
+                              // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   // bf16 inference models (cfg5)
@@ -1189,6 +1273,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
+  if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   {
     StepState s0{};
@@ -1677,9 +1762,28 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     wa.dZ = dz_cur; wa.ldz = dz_pk ? ly.N : ld_dy; wa.zpk = dz_pk;
     wa.M = (int)B; wa.K = ly.K; wa.N = ly.N;
     wa.dW = grads + ly.w; wa.db = grads + ly.b;
-    int rc = launch_wgrad(m, wa, st);
-    if (rc) return rc;
-    if (l == 0) break;
+    const bool fuse = m->fuse_adam != nullptr;
+    if (fuse) {
+      // single-GPU train step: Adam where the gradient is formed.  W(l) is read by dgrad(l),
+      // so dW + Adam(l) runs after it; the previous layer's gamma/beta (read by dgrad(l) and
+      // k_bn_bwd) are updated here too, from the gradients k_bn_bwd stored.
+      wa.adam = 1; wa.af = *m->fuse_adam;
+      wa.w = m->flat[0]; wa.m = m->flat[2]; wa.v = m->flat[3]; wa.woff = ly.w; wa.boff = ly.b;
+      wa.wd = m->wpk + ly.wd; wa.wf = m->wpk + ly.wf;
+      if (l >= 1 && m->layers[l - 1].bn) {
+        wa.bn_adam = 1; wa.gflat = grads; wa.goff = m->layers[l - 1].gamma; wa.btoff = m->layers[l - 1].beta;
+      }
+    } else {
+      int rc = launch_wgrad(m, wa, st);
+      if (rc) return rc;
+    }
+    if (l == 0) {
+      if (fuse) {
+        int rc = launch_wgrad(m, wa, st);
+        if (rc) return rc;
+      }
+      break;
+    }
     const Layer& pv = m->layers[l - 1];
     BwdArgs a{};
     a.dZ = dz_cur; a.ldz = dz_pk ? ly.N : ld_dy;
@@ -1743,6 +1847,10 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       LAUNCH_CHECK("k_dgrad");
     }
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
+    if (fuse) {
+      int rc = launch_wgrad(m, wa, st);
+      if (rc) return rc;
+    }
     dz_cur = m->dz[l - 1];
     dz_pk = true;
   }
@@ -1775,6 +1883,35 @@ extern "C" int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, i
   rc = p3d_backward(m, m->dybuf, B, stream);
   m->loss_dst = nullptr;
   return rc;
+}
+
+// One whole single-GPU TF1 training step (session.run([updates, loss, ...]),
+// linear_model.py:225-237): forward + fused MSE + backward with the Adam update applied
+// inside the weight-gradient kernels (no separate optimizer pass, no gradient round trip
+// through HBM), then the step state advances.  --max_norm models (the clip's gradient needs
+// every G first) take the unfused sequence.  lr = lr0 * decay_rate^(global_step/decay_steps).
+static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st);
+
+extern "C" int p3d_train_step(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
+                              float keep_prob, uint64_t seed, float lr0, float decay_steps, float decay_rate,
+                              float* loss_dev, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_train_step: null model");
+  hipStream_t st = (hipStream_t)stream;
+  if (m->cfg.max_norm || !m->train_split || !m->adam_in_wgrad) {
+    int rc = p3d_train_fwd_bwd(m, x, t, B, y, keep_prob, seed, 0, loss_dev, stream);
+    if (rc) return rc;
+    return adam_launch(m, -1.0f, lr0, decay_steps, decay_rate, st);
+  }
+  AdamFuse af{};
+  af.st = m->dstate; af.lr_host = -1.0f; af.lr0 = lr0; af.decay_steps = decay_steps; af.decay_rate = decay_rate;
+  af.b1 = 0.9f; af.b2 = 0.999f; af.eps = 1e-8f;
+  m->fuse_adam = &af;
+  const int rc = p3d_train_fwd_bwd(m, x, t, B, y, keep_prob, seed, 0, loss_dev, stream);
+  m->fuse_adam = nullptr;
+  if (rc) return rc;
+  k_step_advance<<<1, 1, 0, st>>>(m->dstate, af.b1, af.b2);
+  LAUNCH_CHECK("k_step_advance");
+  return P3D_OK;
 }
 
 static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st) {
@@ -1887,6 +2024,43 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
   strncpy(out, n.c_str(), (size_t)out_len - 1);
   out[out_len - 1] = 0;
   return P3D_OK;
+}
+
+// DLPack (v0.8 ABI) alias of device memory for the host binding (torch.from_dlpack):
+// the managed-tensor record and its deleter live here, so freeing the view never calls
+// back into Python (a ctypes-callback deleter crashed interpreter teardown).
+namespace {
+struct DlDevice { int32_t device_type; int32_t device_id; };
+struct DlDType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DlTensor {
+  void* data; DlDevice device; int32_t ndim; DlDType dtype; int64_t* shape; int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DlManaged { DlTensor dl_tensor; void* manager_ctx; void (*deleter)(DlManaged*); };
+void dl_free(DlManaged* t) {
+  if (!t) return;
+  free(t->dl_tensor.shape);
+  free(t);
+}
+}  // namespace
+
+extern "C" void* p3d_dlpack_alias(void* data, int32_t ndim, const int64_t* shape, int32_t device_id,
+                                  int32_t dtype_code, int32_t bits) {
+  if (ndim <= 0 || !shape) return nullptr;
+  DlManaged* t = (DlManaged*)calloc(1, sizeof(DlManaged));
+  if (!t) return nullptr;
+  t->dl_tensor.shape = (int64_t*)malloc(sizeof(int64_t) * (size_t)ndim);
+  if (!t->dl_tensor.shape) { free(t); return nullptr; }
+  for (int i = 0; i < ndim; ++i) t->dl_tensor.shape[i] = shape[i];
+  t->dl_tensor.data = data;
+  t->dl_tensor.device.device_type = 10;   // kDLROCM
+  t->dl_tensor.device.device_id = device_id;
+  t->dl_tensor.ndim = ndim;
+  t->dl_tensor.dtype.code = (uint8_t)dtype_code;
+  t->dl_tensor.dtype.bits = (uint8_t)bits;
+  t->dl_tensor.dtype.lanes = 1;
+  t->deleter = dl_free;
+  return t;
 }
 
 extern "C" int p3d_profile_start(p3d_model* m, int32_t max_launches) {

@@ -27,6 +27,7 @@ struct MpjpeArgs {
 
 // joint j of one frame, un-normalized (mm)
 __device__ __forceinline__ void p3d_joint(const float* row, const MpjpeArgs& a, int j, double v[3]) {
+#pragma clang fp contract(off)   // x*std + mean rounded twice, as numpy computes it
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     if (a.root && j == 0) {
@@ -147,6 +148,7 @@ __global__ __launch_bounds__(64) void k_mpjpe(MpjpeArgs a) {
     }
   }
   if (!PROC) {
+#pragma clang fp contract(off)
     for (int j = 0; j < a.J; ++j) {
       double dist = 0.0;
       if (live) {

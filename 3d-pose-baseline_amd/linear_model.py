@@ -15,16 +15,31 @@ fallback: construction fails if libp3d.so cannot be loaded.
 """
 from __future__ import annotations
 
+import atexit
 import json
 import math
 import os
 import time
+import weakref
 
 import numpy as np
 
 import _p3d
 import dist_utils
 from _p3d import check, lib, ptr
+
+# Models still open at interpreter exit are destroyed here, before the HIP runtime is torn
+# down (a p3d_destroy from a __del__ during teardown has crashed the process).
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_models():
+    for m in list(_LIVE):
+        try:
+            m.close()
+        except Exception:
+            pass
 
 HUMAN_2D_SIZE = 16 * 2
 
@@ -176,6 +191,7 @@ class LinearModel(object):
         with torch.cuda.device(self.device):
             check(lib().p3d_create(_p3d.ctypes.byref(cfg), _p3d.ctypes.byref(h)), "p3d_create")
         self._h = h
+        _LIVE.add(self)
         self._tables()
 
         # placeholders / tensors the reference exposes (src/linear_model.py:77-134)
@@ -402,17 +418,21 @@ class LinearModel(object):
         if out is None:
             out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
         y = out
-        # forward + fused MSE + backward in one call; the dropout counter, lr decay and the
-        # Adam beta powers all come from the device-side step state, so this sequence is
-        # capturable in a HIP graph
-        check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
-                                      self.rank * B, ptr(self._loss_dev), self.stream()), "p3d_train_fwd_bwd")
-        loss = self._loss_dev
-        if self.data_parallel:
+        # the dropout counter, lr decay and the Adam beta powers all come from the device-side
+        # step state, so either sequence is capturable in a HIP graph
+        if not self.data_parallel:
+            # one call: forward + fused MSE + backward with Adam inside the gradient kernels
+            check(lib().p3d_train_step(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
+                                       self.lr0, 100000.0, 0.96, ptr(self._loss_dev), self.stream()),
+                  "p3d_train_step")
+        else:
+            # forward + fused MSE + backward, all-reduce of the flat gradient, TF1 Adam
+            check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
+                                          self.rank * B, ptr(self._loss_dev), self.stream()), "p3d_train_fwd_bwd")
             self._allreduce_grads()
-        check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
+            check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
         self._step_host += 1
-        return loss, y
+        return self._loss_dev, y
 
     def compute_gradients(self, x, t, keep_prob, ctr=None):
         """Forward (training) + MSE + backward, no optimizer update (opt.compute_gradients,

@@ -121,6 +121,18 @@ int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, f
                       float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,
                       void* stream);
 
+/* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
+ * the TF1 Adam update, global_step += 1.  With env P3D_FUSE_ADAM=1 at p3d_create the update
+ * runs inside the weight-gradient kernels instead (no separate optimizer pass; the flat
+ * grads buffer then holds the bias and BN gradients, not dW), bit-identical to the unfused
+ * sequence (tests/test_gpu_parity.py) but slower at cfg3.
+ * lr = lr0 * decay_rate^(global_step / decay_steps) on the device.  Equivalent to
+ * p3d_train_fwd_bwd + p3d_adam_step_decay (which --max_norm models use internally).
+ * Graph-capturable; data-parallel training uses the unfused calls around its all-reduce. */
+int p3d_train_step(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
+                   float keep_prob, uint64_t seed, float lr0, float decay_steps, float decay_rate,
+                   float* loss_dev, void* stream);
+
 /* One TF1 ApplyAdam over all trainables (linear_model.py:137,145):
  *   alpha = lr*sqrt(1-beta2_power)/(1-beta1_power); m += (g-m)(1-b1);
  *   v += (g^2-v)(1-b2); w -= (m*alpha)/(sqrt(v)+eps)
@@ -161,6 +173,12 @@ int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const 
  * 0 = inference hidden layer at B <= 64, 1 = inference hidden layer at large M,
  * 2 = BN-train hidden-layer GEMM.  (Measurement plumbing for bench.py.) */
 int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len);
+
+/* Host-binding plumbing: a DLPack v0.8 DLManagedTensor aliasing `data` (no copy; the
+ * memory stays owned by its model), with a C deleter that frees only the record.  Wrap
+ * it in a "dltensor" PyCapsule for torch.utils.dlpack.from_dlpack.  NULL on bad input. */
+void* p3d_dlpack_alias(void* data, int32_t ndim, const int64_t* shape, int32_t device_id,
+                       int32_t dtype_code, int32_t bits);
 
 /* Live kernel timing (bench.py's roofline): while active, every kernel the model
  * launches is bracketed by a hipEvent pair.  p3d_profile_stop synchronises and writes

@@ -187,6 +187,44 @@ def test_predict14_gradients_and_train_steps():
     m.close()
 
 
+@pytest.mark.parametrize("residual,batch_norm", [(True, True), (False, False), (True, False)])
+def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, monkeypatch):
+    """p3d_train_step with Adam inside the gradient kernels (P3D_FUSE_ADAM=1) ==
+    p3d_train_fwd_bwd + p3d_adam_step_decay, bit for bit, over 4 steps (weights, slots,
+    moving stats, step)."""
+    import _p3d
+    monkeypatch.setenv("P3D_FUSE_ADAM", "1")
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=residual, batch_norm=batch_norm)
+    st = ref_mlp.init_state(cfg, seed=4, bn_seed=5)
+    ms = []
+    for _ in range(2):
+        m = linear_model.LinearModel(256, 2, residual, batch_norm, False, 64, 1e-3, "/tmp/p3d_test", seed=9)
+        m.set_weights({**st.params, **st.moving})
+        ms.append(m)
+    fused, plain = ms
+    rng = np.random.default_rng(3)
+    for step in range(4):
+        x = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+        t = torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda()
+        yf = torch.empty((64, 48), device="cuda")
+        yp = torch.empty((64, 48), device="cuda")
+        fused.train_step_device(x, t, 0.5, out=yf)
+        _p3d.check(_p3d.lib().p3d_train_fwd_bwd(plain._h, x.data_ptr(), t.data_ptr(), 64, yp.data_ptr(), 0.5,
+                                                 plain.seed, 0, plain._loss_dev.data_ptr(), plain.stream()), "fb")
+        _p3d.check(_p3d.lib().p3d_adam_step_decay(plain._h, plain.lr0, 100000.0, 0.96, plain.stream()), "adam")
+        assert torch.equal(yf, yp), step
+        assert torch.equal(fused._loss_dev, plain._loss_dev), step
+    for k in ("params", "moving", "adam_m", "adam_v"):
+        if fused.flat[k] is not None:
+            assert torch.equal(fused.flat[k], plain.flat[k]), k
+    assert fused.get_step() == plain.get_step()
+    # the packed forward copies were re-packed by the fused kernels: the next forward agrees
+    x = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+    assert torch.equal(fused.forward_device(x), plain.forward_device(x))
+    fused.close()
+    plain.close()
+
+
 def test_mpjpe_kernel_matches_reference_goldens():
     g = np.load("tests/golden/reference_goldens.npz", allow_pickle=False)
     st, m = make(ref_mlp.Cfg(linear_size=256, num_layers=1))
