@@ -186,7 +186,11 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   const bool cok = col < p.N;
   const int cc = cok ? col : p.N - 1;
   const int ngN = (p.N + 15) >> 4;
-  const bool trace = (RS == 4 && KIND == 1 && w == 0);
+#ifndef P3D_TRACE_RS
+#define P3D_TRACE_RS 4
+#endif
+  const bool trace = (RS == P3D_TRACE_RS && KIND == 1 && w == 0);
+  const bool trace_last = (RS == P3D_TRACE_RS && KIND == 1 && w == WK - 1);
   if (trace) P3D_STAMP(0);
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
@@ -212,6 +216,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
   p3d_core<RS, DEPTH, NACC, APK>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
   if (trace) P3D_STAMP(1);
+  if (trace_last) P3D_STAMP(6);
   if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
   if (trace) P3D_STAMP(2);
   // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r of column n0+i ---------------
@@ -326,6 +331,94 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       else p.Y[(int64_t)row * p.ldy + col] = y;
     }
   if (trace) P3D_STAMP(5);
+}
+
+// =====================================================================================
+// Inference layer in the transposed-accumulator form (p3d_core SWAP): lane (i, q) ends
+// holding row 16s + i, columns n0 + 4q .. +3 -- one float4 per operand of the epilogue
+// (bias, eval BN, residual, packed output: one 1 KB wave store per tile) and one Philox
+// block per lane for dropout.  Same contraction and reduction order as k_fwd (the
+// transposed MFMA sums the same products in the same order), so results are identical.
+// =====================================================================================
+template <int RS, int WK, int DEPTH, int NACC, bool APK, bool YPK, int KIND>
+__global__ __launch_bounds__(64 * WK) void k_fwd_t(FwdArgs p) {
+  __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int ct = blockIdx.x, m0 = blockIdx.y * 16 * RS;
+  const int n0 = ct * 16 + 4 * q;                 // this lane's first column
+  const int ngN = (p.N + 15) >> 4;
+  const bool vec = (p.N & 3) == 0 && n0 + 3 < p.N;
+  // epilogue operands (per-column float4s, per-tile residual) issued before the GEMM
+  f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f}, inv4 = f32x4{1.f, 1.f, 1.f, 1.f}, sh4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rv[RS];
+  uint64_t ctr = p.ctr;
+  if (w == 0) {
+    if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
+    f32x4 g4 = inv4, be4 = sh4, mu4 = sh4, va4 = inv4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = n0 + e < p.N ? n0 + e : p.N - 1;
+      b4[e] = p.bias[c];
+      if (p.bn) { g4[e] = p.gamma[c]; be4[e] = p.beta[c]; mu4[e] = p.mmean[c]; va4[e] = p.mvar[c]; }
+    }
+    if (p.bn) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        inv4[e] = (1.0f / sqrtf(va4[e] + p.eps)) * g4[e];
+        sh4[e] = be4[e] - mu4[e] * inv4[e];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+      const int rt = (m0 >> 4) + s;
+      rv[s] = p.res ? *(const f32x4*)(p.res + ((int64_t)rt * ngN + ct) * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const int ngt = p.K >> 4;
+  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
+  f32x4 acc[NACC][RS];
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_core<RS, DEPTH, NACC, APK, true>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
+  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
+  const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
+#pragma unroll
+  for (int s = 0; s < RS; ++s) {
+    const int row = m0 + 16 * s + i;
+    float u[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.keep < 1.0f) {
+      const uint4 wq = p3d_philox(make_uint4((uint32_t)(p.row_off + row), (uint32_t)(n0 >> 2), (uint32_t)p.site,
+                                             (uint32_t)ctr), (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      const uint32_t xs[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = __uint_as_float((xs[e] & 0x7FFFFFu) | 0x3F800000u) - 1.0f;
+    }
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = (p.wsq ? acc[0][s][e] / mx : acc[0][s][e]) + b4[e];
+      float y = p.bn ? z * inv4[e] + sh4[e] : z;
+      if (p.relu) y = fmaxf(y, 0.0f);
+      if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, u[e]);
+      if (p.res) y += rv[s][e];
+      o[e] = y;
+    }
+    if (YPK) {
+      // whole tile rows (padding rows included) -- the packed buffers hold them
+      *(f32x4*)(p.Y + ((int64_t)((m0 >> 4) + s) * ngN + ct) * 256 + lane * 4) = o;
+    } else if (row < p.M) {
+      if (vec && ((p.ldy & 3) == 0)) {
+        *(f32x4*)(p.Y + (int64_t)row * p.ldy + n0) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n0 + e < p.N) p.Y[(int64_t)row * p.ldy + n0 + e] = o[e];
+      }
+    }
+  }
 }
 
 // =====================================================================================
@@ -1058,6 +1151,8 @@ struct p3d_model {
   // workgroups co-reside per CU, so independent batches on different streams overlap
   // (tools/streams_sweep2.py: 4 streams 5.6 M poses/s vs 4.9 M with 16-wave workgroups).
   int infer_wk = 82;        // inference tiling variant (launch_fwd_k), env P3D_INFER_WK
+  int fwd_t = 0;            // inference layers in the transposed-accumulator form (env P3D_FWD_T=1;
+                            // bit-identical, +3% single-stream, -2% at 4 streams: 58 vs 52 VGPRs)
   int in_wk = 2, out_wk = 16; // input / output layer variants (env P3D_IN_WK, P3D_OUT_WK; 0 = infer_wk)
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
@@ -1269,6 +1364,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if ((e = hipMemset(m->scratch, 0, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev);
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_FWD_T")) m->fwd_t = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
@@ -1501,8 +1597,17 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   int wk = whole_batch ? m->train_wk : m->infer_wk;
   if (!whole_batch && kind == 0 && m->in_wk) wk = m->in_wk;
   if (!whole_batch && kind == 2 && m->out_wk) wk = m->out_wk;
+  const dim3 g16((a.N + 15) / 16, (a.M + 15) / 16);
+  if (m->fwd_t && !whole_batch && (a.bn == 0 || a.bn == 1) && !a.z_save && !a.tgt && wk == (kind == 0 ? 2 : kind == 1 ? 82 : 16)) {
+    // inference, transposed-accumulator form (float4 epilogue, 1 KB tile stores)
+    if (kind == 0) go(ps, k_fwd_t<1, 2, 1, 2, false, true, 0>, g16, dim3(128), st, a);
+    else if (kind == 1) go(ps, k_fwd_t<1, 8, 2, 2, true, true, 1>, g16, dim3(512), st, a);
+    else go(ps, k_fwd_t<1, 16, 4, 2, true, false, 2>, g16, dim3(1024), st, a);
+    LAUNCH_CHECK("k_fwd_t");
+    return P3D_OK;
+  }
   if (kind == 0 && wk == 2) {   // K = 32: one k-group per wave
-    go(ps, k_fwd<1, 2, 1, 2, false, true, 0>, dim3((a.N + 15) / 16, (a.M + 15) / 16), dim3(128), st, a);
+    go(ps, k_fwd<1, 2, 1, 2, false, true, 0>, g16, dim3(128), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
   }
@@ -2000,7 +2105,9 @@ extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const dou
 extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len) {
   if (!m || !out || out_len <= 0) return fail(P3D_ERR_ARG, "p3d_kernel_name: bad argument");
   std::string n;
-  if (what == 0) {
+  if (what == 0 && m->fwd_t && m->infer_wk == 82) {
+    n = "k_fwd_t<1, 8, 2, 2, true, true, 1>";
+  } else if (what == 0) {
     switch (m->infer_wk) {
       case 8: n = "k_fwd<1, 8, 8, 2, true, true, 1>"; break;
       case 84: n = "k_fwd<1, 8, 4, 2, true, true, 1>"; break;

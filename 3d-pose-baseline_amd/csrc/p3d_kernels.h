@@ -87,7 +87,10 @@ __device__ __forceinline__ float p3d_dropout_mask(float keep, float u) { return 
 //   APK = false: A row-major with leading dimension lda (rows clamped to M-1)
 //   B always packed (ngB groups per column tile)
 // ------------------------------------------------------------------------------------
-template <int RS, int DEPTH, int NACC, bool APK>
+// SWAP = true computes the transposed product (B fragment as the MFMA A operand): the
+// accumulator of lane (i, q) then holds row 16s + i, columns 4q .. 4q+3 of the tile (the
+// fragment-major layout itself) instead of column i, rows 4q .. 4q+3.
+template <int RS, int DEPTH, int NACC, bool APK, bool SWAP = false>
 __device__ __forceinline__ void p3d_core(const float* __restrict__ A, int64_t lda, int ngA, int M, int m0,
                                          const float* __restrict__ Bp, int ngB, int ct, int gb, int ge,
                                          f32x4 (&acc)[NACC][RS]) {
@@ -124,7 +127,8 @@ __device__ __forceinline__ void p3d_core(const float* __restrict__ A, int64_t ld
         for (int e = 0; e < 4; ++e)
 #pragma unroll
           for (int s = 0; s < RS; ++s)
-            acc[e % NACC][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][s][e], rb[d][e], acc[e % NACC][s], 0, 0, 0);
+            acc[e % NACC][s] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x4f32(rb[d][e], ra[d][s][e], acc[e % NACC][s], 0, 0, 0)
+                                    : __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][s][e], rb[d][e], acc[e % NACC][s], 0, 0, 0);
         if (gi + DEPTH < ng) {
 #pragma unroll
           for (int s = 0; s < RS; ++s) ra[d][s] = pa[s][(gi + DEPTH) * ASTR];

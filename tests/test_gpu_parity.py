@@ -88,6 +88,20 @@ def test_eval_forward_large_batch(B, residual, batch_norm, max_norm, keep):
     m.close()
 
 
+@pytest.mark.parametrize("B,keep,max_norm", [(64, 1.0, False), (37, 0.5, False), (64, 1.0, True)])
+def test_transposed_inference_kernels_bit_identical(B, keep, max_norm, monkeypatch):
+    """k_fwd_t (transposed accumulator, float4 epilogue) == k_fwd, bit for bit."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True, max_norm=max_norm)
+    ys = []
+    x = torch.from_numpy(np.random.default_rng(B).standard_normal((B, 32)).astype(np.float32)).cuda()
+    for flag in ("1", "0"):
+        monkeypatch.setenv("P3D_FWD_T", flag)
+        st, m = make(cfg, batch=B, max_batch=64)
+        ys.append(m.forward_device(x, False, keep, ctr=7).cpu())
+        m.close()
+    assert torch.equal(ys[0], ys[1])
+
+
 def _grad_check(cfg, keep, B=64):
     st, m = make(cfg, batch=B)
     rng = np.random.default_rng(9)
