@@ -403,7 +403,7 @@ class LinearModel(object):
                             0 if dy is None else ptr(dy), self.stream()), "p3d_mse")
         return self._loss_dev
 
-    def train_step_device(self, x, t, keep_prob, out=None):
+    def train_step_device(self, x, t, keep_prob, out=None, loss_out=None):
         """One TF1 training step (fwd + MSE + bwd + [all-reduce] + Adam), device resident.
 
         Returns (loss_device_scalar, outputs).  Mirrors session.run([updates, loss, ...])
@@ -420,19 +420,20 @@ class LinearModel(object):
         y = out
         # the dropout counter, lr decay and the Adam beta powers all come from the device-side
         # step state, so either sequence is capturable in a HIP graph
+        loss_t = self._loss_dev if loss_out is None else loss_out
         if not self.data_parallel:
             # one call: forward + fused MSE + backward with Adam inside the gradient kernels
             check(lib().p3d_train_step(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
-                                       self.lr0, 100000.0, 0.96, ptr(self._loss_dev), self.stream()),
+                                       self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
                   "p3d_train_step")
         else:
             # forward + fused MSE + backward, all-reduce of the flat gradient, TF1 Adam
             check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
-                                          self.rank * B, ptr(self._loss_dev), self.stream()), "p3d_train_fwd_bwd")
+                                          self.rank * B, ptr(loss_t), self.stream()), "p3d_train_fwd_bwd")
             self._allreduce_grads()
             check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
         self._step_host += 1
-        return self._loss_dev, y
+        return loss_t, y
 
     def compute_gradients(self, x, t, keep_prob, ctr=None):
         """Forward (training) + MSE + backward, no optimizer update (opt.compute_gradients,

@@ -59,6 +59,9 @@ def build_parser():
     p.add_argument("--synthetic", action='store_true', default=False,
                    help="Use synthetic H3.6M-shaped data (the dataset is not part of this build)")
     p.add_argument("--seed", type=int, default=0, help="Weight / dropout seed")
+    p.add_argument("--device_loop", type=int, default=1,
+                   help="1: stage each epoch in HBM and train without per-step host round trips; "
+                        "0: the reference's per-batch step() loop")
     return p
 
 
@@ -286,8 +289,14 @@ def synthetic_h36m(n_train=20000, n_test=4000, seed=0, out_dim=48):
             for j, subj in enumerate(subjects):
                 k = max(1, n // (len(actions) * len(subjects)))
                 x = rng.standard_normal((k + j * 7, 32))
-                s2[(subj, a, "%s.%d.h5" % (a, j))] = x
-                s3[(subj, a, "%s.%d.h5" % (a, j))] = np.tanh(x @ proj) + 0.1 * rng.standard_normal((len(x), out_dim))
+                y = np.tanh(x @ proj) + 0.1 * rng.standard_normal((len(x), out_dim))
+                # H3.6M key shapes: 2D (and camera-frame 3D) "<seq>.<camera>.h5", world-frame
+                # 3D "<seq>.h5" -- get_all_batches derives the 3D key from the 2D one
+                # (src/linear_model.py:272-273); one camera per sequence, so both resolve
+                seq = "%s %d" % (a, j)
+                s2[(subj, a, "%s.54138969.h5" % seq)] = x
+                s3[(subj, a, "%s.54138969.h5" % seq)] = y
+                s3[(subj, a, "%s.h5" % seq)] = y
         return s2, s3
 
     tr2, tr3 = make(data_utils.TRAIN_SUBJECTS, n_train)
@@ -323,18 +332,43 @@ def train(flags=None):
             nbatches = len(enc)
             print("There are {0} train batches".format(nbatches))
             start_time, loss = time.time(), 0.
-            for i in range(nbatches):
-                step_loss, loss_summary, lr_summary, _ = model.step(sess, enc[i], dec[i], flags.dropout,
-                                                                    isTraining=True)
-                if (i + 1) % log_every_n_batches == 0:
-                    model.train_writer.add_summary(loss_summary, current_step)
-                    model.train_writer.add_summary(lr_summary, current_step)
-                    step_time = time.time() - start_time
-                    start_time = time.time()
-                    print("Working on epoch {0}, batch {1} / {2}... done in {3:.2f} ms".format(
-                        epoch, i + 1, nbatches, 1000 * step_time / log_every_n_batches))
-                loss += step_loss
-                current_step += 1
+            if flags.device_loop:
+                # the epoch's batches staged in HBM once; per-step losses land in a device
+                # vector (no host round trip per step; one sync per logging interval)
+                import torch
+                B = flags.batch_size
+                with torch.cuda.device(model.device):
+                    X = torch.from_numpy(_stack(enc, model.input_size)).to(model.device)
+                    T = torch.from_numpy(_stack(dec, model.output_size)).to(model.device)
+                    losses = torch.zeros(max(nbatches, 1), dtype=torch.float32, device=model.device)
+                    for i in range(nbatches):
+                        lr = linear_model.exponential_decay(model.lr0, model._step_host)
+                        model.train_step_device(X[i * B:(i + 1) * B], T[i * B:(i + 1) * B], flags.dropout,
+                                                loss_out=losses[i:i + 1])
+                        if (i + 1) % log_every_n_batches == 0:
+                            step_loss = float(losses[i].item())
+                            model.train_writer.add_summary(linear_model.Summary("loss/loss", step_loss), current_step)
+                            model.train_writer.add_summary(
+                                linear_model.Summary("learning_rate/learning_rate", lr), current_step)
+                            step_time = time.time() - start_time
+                            start_time = time.time()
+                            print("Working on epoch {0}, batch {1} / {2}... done in {3:.2f} ms".format(
+                                epoch, i + 1, nbatches, 1000 * step_time / log_every_n_batches))
+                        current_step += 1
+                    loss = float(losses[:nbatches].double().sum().item())
+            else:
+                for i in range(nbatches):
+                    step_loss, loss_summary, lr_summary, _ = model.step(sess, enc[i], dec[i], flags.dropout,
+                                                                        isTraining=True)
+                    if (i + 1) % log_every_n_batches == 0:
+                        model.train_writer.add_summary(loss_summary, current_step)
+                        model.train_writer.add_summary(lr_summary, current_step)
+                        step_time = time.time() - start_time
+                        start_time = time.time()
+                        print("Working on epoch {0}, batch {1} / {2}... done in {3:.2f} ms".format(
+                            epoch, i + 1, nbatches, 1000 * step_time / log_every_n_batches))
+                    loss += step_loss
+                    current_step += 1
             loss = loss / max(nbatches, 1)
             print("=============================\n"
                   "Global step:         %d\n"
