@@ -143,6 +143,16 @@ class Saver:
                 os.remove(old + ".npz")
         return path
 
+    def save_npy_dump(self, session, directory, all_variables=False):
+        """The reference's per-variable npy export (src/predict_3dpose.py:548-568)."""
+        import checkpoint_io
+        return checkpoint_io.export_npy_dump(self.model, directory, all_variables)
+
+    def restore_npy_dump(self, session, directory):
+        """Load a reference npy-dump directory (trainable or global variables)."""
+        import checkpoint_io
+        return checkpoint_io.import_npy_dump(self.model, directory)
+
     def restore(self, session, save_path):
         p = save_path if save_path.endswith(".npz") else save_path + ".npz"
         if not os.path.exists(p):

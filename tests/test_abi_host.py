@@ -146,3 +146,25 @@ def test_session_shim_summary():
     ph = linear_model.Placeholder("error_mm")
     out = s.run(("summary", "loss/error_mm"), {ph: 12.5})
     assert out.tag == "loss/error_mm" and out.value == 12.5
+
+
+def test_checkpoint_io_names_and_order():
+    """TF1 global-variable order and the reference's npy-dump file names
+    (src/predict_3dpose.py:548-568) -- host logic only."""
+    import checkpoint_io as cio
+    table = [("linear_model/w1", 32 * 256, 0, 0), ("linear_model/b1", 256, 0, 8192),
+             ("linear_model/batch_normalization/gamma", 256, 0, 8448),
+             ("linear_model/batch_normalization/beta", 256, 0, 8704),
+             ("linear_model/batch_normalization/moving_mean", 256, 1, 0),
+             ("linear_model/batch_normalization/moving_variance", 256, 1, 256),
+             ("linear_model/w4", 256 * 48, 0, 8960), ("linear_model/b4", 48, 0, 21248)]
+    g = cio.global_order(table)
+    assert g[:4] == ["learning_rate", "global_step", "linear_model/w1", "linear_model/b1"]
+    assert g.index("linear_model/batch_normalization/moving_mean") == 6
+    assert g[g.index("beta1_power") + 1] == "beta2_power"
+    assert g[-2:] == ["linear_model/b4/Adam", "linear_model/b4/Adam_1"]
+    assert cio.trainable_order(table) == [n for n, _, k, _ in table if k == 0]
+    f = cio.dump_filename(7, "linear_model/batch_normalization/gamma")
+    assert f == "0007 - linear_model-batch_normalization-gamma:0.npy"
+    assert cio.parse_dump_filename(f) == (7, "linear_model/batch_normalization/gamma")
+    assert cio.parse_dump_filename("notes.txt") is None

@@ -9,6 +9,8 @@ Tolerances (fp32 path vs fp64 oracle):
   analytically zero under batch-norm and Adam normalises its rounding noise
   (DESIGN.md, "pre-BN bias").
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -237,6 +239,33 @@ def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, monkeyp
     assert torch.equal(fused.forward_device(x), plain.forward_device(x))
     fused.close()
     plain.close()
+
+
+def test_npy_dump_round_trip(tmp_path):
+    """Reference npy-dump export / import (trainable and global variables)."""
+    import checkpoint_io
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    rng = np.random.default_rng(1)
+    for _ in range(2):
+        m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 0.5, isTraining=True)
+    paths = m.saver.save_npy_dump(None, str(tmp_path / "all"), all_variables=True)
+    m.saver.save_npy_dump(None, str(tmp_path / "tr"))
+    assert os.path.basename(paths[2]) == "0002 - linear_model-w1:0.npy"
+    full = m.get_state()
+    _, m2 = make(cfg, model_seed=99)
+    loaded = m2.saver.restore_npy_dump(None, str(tmp_path / "all"))
+    assert "global_step" in loaded and "linear_model/w1/Adam" in loaded
+    s2 = m2.get_state()
+    for k in full:
+        np.testing.assert_array_equal(np.asarray(full[k]), np.asarray(s2[k]), err_msg=k)
+    _, m3 = make(cfg, model_seed=98)
+    m3.saver.restore_npy_dump(None, str(tmp_path / "tr"))
+    w = m3.get_weights()
+    for k in m.trainable_names():
+        np.testing.assert_array_equal(w[k], full[k], err_msg=k)
+    for mm in (m, m2, m3):
+        mm.close()
 
 
 def test_mpjpe_kernel_matches_reference_goldens():
