@@ -167,6 +167,41 @@ def cpu_baseline(mode, seconds=12.0):
                       % (n, "train-step" if mode == "train" else "inference", dt)}
 
 
+def distinct_queue_streams(n, pool=16, cycles=200_000):
+    """n streams that run concurrently, i.e. are bound to n different hardware queues.
+
+    HIP binds each stream to one of GPU_MAX_HW_QUEUES queues at first use; which one is not
+    a function of creation order we can rely on (tools/dispatch_probe.hip: of streams 0..3
+    only two ran concurrently, of 0, 2, 4, 6 all four).  So the binding is observed: a
+    candidate joins when a spin kernel on it overlaps one on every stream already chosen."""
+    import torch
+    cands = [torch.cuda.Stream() for _ in range(pool)]
+    for st in cands:
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(10)
+    torch.cuda.synchronize()
+
+    def spin_time(streams):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for st in streams:
+            with torch.cuda.stream(st):
+                torch.cuda._sleep(cycles)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    t1 = min(spin_time([cands[0]]) for _ in range(3))
+    chosen = [cands[0]]
+    for c in cands[1:]:
+        if len(chosen) == n:
+            break
+        if all(min(spin_time([c, d]) for _ in range(2)) < 1.5 * t1 for d in chosen):
+            chosen.append(c)
+    if len(chosen) < n:
+        chosen += [c for c in cands if c not in chosen][:n - len(chosen)]
+    return chosen
+
+
 def bench_infer(args, rank, world):
     """K forward steps of one 64-pose batch each.  S streams (one per hardware queue) each
     replay their own HIP graph of G/S steps over a disjoint workspace slot
@@ -194,14 +229,18 @@ def bench_infer(args, rank, world):
     # round robin; the first pool streams share queues with torch's own, so one round of
     # streams is touched first and the batch streams land on 4 distinct idle queues
     # (tools/streams_probe.py: 3.8 -> 5.6 M poses/s at 4 streams).
-    spare = [torch.cuda.Stream() for _ in range(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))]
-    for st in spare:
-        with torch.cuda.stream(st):
-            torch.zeros(16, device="cuda").add_(1)
-    torch.cuda.synchronize()
+    if args.queue_probe:
+        pool = distinct_queue_streams(S)
+    else:
+        spare = [torch.cuda.Stream() for _ in range(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))]
+        for st in spare:
+            with torch.cuda.stream(st):
+                torch.zeros(16, device="cuda").add_(1)
+        torch.cuda.synchronize()
+        pool = None
 
     def capture(nstreams):
-        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+        streams = pool[:nstreams] if pool is not None else [torch.cuda.Stream() for _ in range(nstreams)]
         counts = [G // nstreams + (1 if j < G % nstreams else 0) for j in range(nstreams)]
         first = [sum(counts[:j]) for j in range(nstreams)]
         graphs = []
@@ -519,6 +558,8 @@ def main():
     ap.add_argument("--mode", choices=["infer", "train", "eval", "stress"], default="infer")
     ap.add_argument("--graph-steps", type=int, default=240)
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
+    ap.add_argument("--queue-probe", type=int, default=0,
+                    help="pick the inference streams by observed hardware-queue concurrency")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
