@@ -192,6 +192,14 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   const bool trace = (RS == P3D_TRACE_RS && KIND == 1 && w == 0);
   const bool trace_last = (RS == P3D_TRACE_RS && KIND == 1 && w == WK - 1);
   if (trace) P3D_STAMP(0);
+#ifdef P3D_TRACE_PROBE  // first-touch latency of the activations (wave 1 only)
+  if (RS == P3D_TRACE_RS && KIND == 1 && w == 1) {
+    const float v = __builtin_nontemporal_load(p.X + lane * 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (v == 12345.678f) p.Y[0] = v;
+    P3D_STAMP(7);
+  }
+#endif
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
   uint64_t ctr = p.ctr;
@@ -331,6 +339,9 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       else p.Y[(int64_t)row * p.ldy + col] = y;
     }
   if (trace) P3D_STAMP(5);
+#ifdef P3D_TRACE_PROBE  // stores complete (slot 4: the dropout stamp, unused in inference)
+  if (trace) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); P3D_STAMP(4); }
+#endif
 }
 
 // =====================================================================================

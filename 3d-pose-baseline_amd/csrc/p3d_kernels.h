@@ -130,9 +130,15 @@ __device__ __forceinline__ void p3d_core(const float* __restrict__ A, int64_t ld
             acc[e % NACC][s] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x4f32(rb[d][e], ra[d][s][e], acc[e % NACC][s], 0, 0, 0)
                                     : __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][s][e], rb[d][e], acc[e % NACC][s], 0, 0, 0);
         if (gi + DEPTH < ng) {
+#ifndef P3D_DIAG_GA  // diagnostic builds only (tools/): re-read group d instead of streaming
+#define P3D_DIAG_GA(g) (g)
+#endif
+#ifndef P3D_DIAG_GB
+#define P3D_DIAG_GB(g) (g)
+#endif
 #pragma unroll
-          for (int s = 0; s < RS; ++s) ra[d][s] = pa[s][(gi + DEPTH) * ASTR];
-          rb[d] = pb[(gi + DEPTH) * 64];
+          for (int s = 0; s < RS; ++s) ra[d][s] = pa[s][P3D_DIAG_GA(gi + DEPTH) * ASTR];
+          rb[d] = pb[P3D_DIAG_GB(gi + DEPTH) * 64];
         }
       }
     }

@@ -27,7 +27,11 @@ buf = np.zeros(4096 * 8, np.uint64)
 assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
 t = buf.reshape(4096, 8)[:256].astype(np.int64)   # 64 x 4 workgroups of the last hidden launch
 t0 = t[:, 0].min()
-for k, n in [(0, "start"), (1, "gemm w0"), (6, "gemm w7"), (2, "reduced"), (3, "epi"), (5, "stored")]:
+probe = os.environ.get("P3D_TRACE_PROBE") == "1"   # library built with -DP3D_TRACE_PROBE
+phases = [(0, "start")] + ([(7, "X landed")] if probe else []) + \
+    [(1, "gemm w0"), (6, "gemm w7"), (2, "reduced"), (3, "epi"), (5, "stored")] + \
+    ([(4, "drained")] if probe else [])
+for k, n in phases:
     d = (t[:, k] - t0) * 10.0 / 1000.0
     print("%-9s min %6.2f  med %6.2f  max %6.2f us" % (n, d.min(), np.median(d), d.max()))
 model.close()
