@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("P3D_LIB", os.path.join(HERE, "libp3d.so"))  # P3D_LIB
 P3D_CTR_GLOBAL_STEP = 0xFFFFFFFFFFFFFFFF
 P3D_DTYPE_F32 = 0
 P3D_DTYPE_BF16 = 1
+P3D_DTYPE_F64 = 2
 
 
 class P3DCfg(ctypes.Structure):
@@ -64,6 +65,16 @@ SIGNATURES = [
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),
     ("p3d_profile_stop", c_int32, [c_void_p, c_char_p, c_int64]),
     ("p3d_time_layer", c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p]),
+    ("p3d_cam_transform", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    ("p3d_cam_project", c_int32, [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
+    ("p3d_root_center", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
+    ("p3d_normalize", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                c_int32, c_void_p]),
+    ("p3d_unnormalize", c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                  c_void_p, c_void_p]),
+    ("p3d_moments_workspace", c_int64, [c_int64, c_int32]),
+    ("p3d_moments", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
 ]
 
 

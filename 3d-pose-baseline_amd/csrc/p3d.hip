@@ -18,6 +18,7 @@
 #include "p3d_bf16.h"
 #include "p3d_eval.h"
 #include "p3d_gemm.h"
+#include "p3d_data.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -2226,4 +2227,100 @@ extern "C" int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len) {
   m->ev_tag.clear();
   m->ev_used = 0;
   return P3D_OK;
+}
+
+// =====================================================================================
+// H3.6M data pipeline (p3d_data.h)
+// =====================================================================================
+static int64_t p3d_moments_blocks(int64_t F) {
+  int64_t g = (F + 511) / 512;
+  return g < 1 ? 1 : (g > 2048 ? 2048 : g);
+}
+
+extern "C" int p3d_cam_transform(const double* P, int64_t n, int64_t in_cam_stride, const double* cams,
+                                 int32_t C, int32_t inverse, double* out, void* stream) {
+  if (n < 0 || C < 0) return fail(P3D_ERR_ARG, "p3d_cam_transform: negative size");
+  if (n == 0 || C == 0) return 0;
+  if (!P || !cams || !out) return fail(P3D_ERR_ARG, "p3d_cam_transform: null argument");
+  if (in_cam_stride != 0 && in_cam_stride < 3 * n) return fail(P3D_ERR_ARG, "p3d_cam_transform: in_cam_stride < 3n");
+  if (in_cam_stride == 0 && inverse == 0 && (const double*)out == P) return fail(P3D_ERR_ARG, "p3d_cam_transform: out aliases P");
+  CamArgs a{P, in_cam_stride, n, cams, C, out, nullptr, nullptr, nullptr, nullptr};
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (inverse) k_cam_points<1><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else k_cam_points<0><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  LAUNCH_CHECK("k_cam_points");
+  return 0;
+}
+
+extern "C" int p3d_cam_project(const double* P, int64_t n, const double* cams, int32_t C, double* proj,
+                               double* depth, double* radial, double* tan, double* r2, void* stream) {
+  if (n < 0 || C < 0) return fail(P3D_ERR_ARG, "p3d_cam_project: negative size");
+  if (n == 0 || C == 0) return 0;
+  if (!P || !cams || !proj) return fail(P3D_ERR_ARG, "p3d_cam_project: null argument");
+  CamArgs a{P, 0, n, cams, C, proj, depth, radial, tan, r2};
+  k_cam_points<2><<<dim3((unsigned)((n + 255) / 256)), 256, 0, (hipStream_t)stream>>>(a);
+  LAUNCH_CHECK("k_cam_points");
+  return 0;
+}
+
+extern "C" int p3d_root_center(const double* poses, int64_t F, int32_t width, double* out, double* root,
+                               void* stream) {
+  if (F < 0 || width < 3 || width % 3) return fail(P3D_ERR_ARG, "p3d_root_center: width must be 3 * joints");
+  if (F == 0) return 0;
+  if (!poses || !out) return fail(P3D_ERR_ARG, "p3d_root_center: null argument");
+  if ((const double*)out == poses) return fail(P3D_ERR_ARG, "p3d_root_center: out must not alias poses");
+  const int64_t total = F * width;
+  k_root_center<<<dim3((unsigned)((total + 255) / 256)), 256, 0, (hipStream_t)stream>>>(poses, F, width, out, root);
+  LAUNCH_CHECK("k_root_center");
+  return 0;
+}
+
+extern "C" int p3d_normalize(const double* x, int64_t F, int32_t D, const double* mean, const double* stdv,
+                             const int32_t* dims_to_use, int32_t U, void* out, int32_t out_dtype, void* stream) {
+  if (F < 0 || D <= 0 || U < 0) return fail(P3D_ERR_ARG, "p3d_normalize: bad size");
+  if (out_dtype != P3D_DTYPE_F32 && out_dtype != P3D_DTYPE_F64) return fail(P3D_ERR_ARG, "p3d_normalize: out_dtype F32 or F64");
+  if (F == 0 || U == 0) return 0;
+  if (!x || !mean || !stdv || !dims_to_use || !out) return fail(P3D_ERR_ARG, "p3d_normalize: null argument");
+  const int64_t total = F * U;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (out_dtype == P3D_DTYPE_F32) k_normalize<true><<<grid, 256, 0, (hipStream_t)stream>>>(x, F, D, mean, stdv, dims_to_use, U, out);
+  else k_normalize<false><<<grid, 256, 0, (hipStream_t)stream>>>(x, F, D, mean, stdv, dims_to_use, U, out);
+  LAUNCH_CHECK("k_normalize");
+  return 0;
+}
+
+extern "C" int p3d_unnormalize(const void* xn, int32_t in_dtype, int64_t F, int32_t U, const double* mean,
+                               const double* stdv, const int32_t* dims_to_use, int32_t D, double* out, void* stream) {
+  if (F < 0 || U < 0 || D <= 0 || D > 256 || U > D) return fail(P3D_ERR_ARG, "p3d_unnormalize: need 0 <= U <= D <= 256");
+  if (in_dtype != P3D_DTYPE_F32 && in_dtype != P3D_DTYPE_F64) return fail(P3D_ERR_ARG, "p3d_unnormalize: in_dtype F32 or F64");
+  if (F == 0) return 0;
+  if (!mean || !stdv || !out || (U > 0 && (!xn || !dims_to_use))) return fail(P3D_ERR_ARG, "p3d_unnormalize: null argument");
+  const int64_t total = F * D;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (in_dtype == P3D_DTYPE_F32) k_unnormalize<true><<<grid, 256, 0, (hipStream_t)stream>>>(xn, F, U, mean, stdv, dims_to_use, D, out);
+  else k_unnormalize<false><<<grid, 256, 0, (hipStream_t)stream>>>(xn, F, U, mean, stdv, dims_to_use, D, out);
+  LAUNCH_CHECK("k_unnormalize");
+  return 0;
+}
+
+extern "C" int64_t p3d_moments_workspace(int64_t F, int32_t D) {
+  if (F <= 0 || D <= 0) return 0;
+  return p3d_moments_blocks(F) * (int64_t)D * (int64_t)sizeof(double);
+}
+
+extern "C" int p3d_moments(const double* x, int64_t F, int32_t D, double* mean, double* stdv, void* work,
+                           int64_t work_bytes, void* stream) {
+  if (F <= 0 || D <= 0 || D > 256) return fail(P3D_ERR_ARG, "p3d_moments: need F >= 1 and 1 <= D <= 256");
+  if (!x || !mean || !stdv || !work) return fail(P3D_ERR_ARG, "p3d_moments: null argument");
+  if (work_bytes < p3d_moments_workspace(F, D)) return fail(P3D_ERR_ARG, "p3d_moments: workspace too small");
+  const int64_t G = p3d_moments_blocks(F), chunk = (F + G - 1) / G;
+  const hipStream_t st = (hipStream_t)stream;
+  double* part = (double*)work;
+  const dim3 gf((unsigned)((D + 255) / 256));
+  k_col_partial<1><<<dim3((unsigned)G), 256, 0, st>>>(x, F, D, chunk, nullptr, part);
+  k_col_final<1><<<gf, 256, 0, st>>>(part, (int)G, D, F, mean);
+  k_col_partial<2><<<dim3((unsigned)G), 256, 0, st>>>(x, F, D, chunk, mean, part);
+  k_col_final<2><<<gf, 256, 0, st>>>(part, (int)G, D, F, stdv);
+  LAUNCH_CHECK("k_col_partial");
+  return 0;
 }

@@ -39,6 +39,7 @@ extern "C" {
 
 #define P3D_DTYPE_F32 0
 #define P3D_DTYPE_BF16 1   /* bf16 weights/activations, fp32 accumulate + BN */
+#define P3D_DTYPE_F64 2    /* float64 (data-pipeline entry points only)            */
 
 typedef struct p3d_cfg {
   int32_t linear_size;  /* LinearModel(linear_size)            linear_model.py:35 */
@@ -189,6 +190,54 @@ int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len);
 /* Roofline timing hook: `reps` back-to-back launches of hidden layer `layer`
  * (1 .. 2*num_layers) of the inference forward over workspace rows [0, B). */
 int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * H3.6M data pipeline: float64 like the reference's numpy, row-major,
+ * device pointers, asynchronous on `stream`.  These replace the per-sequence numpy loops of
+ * the loaders; results are bit-identical to the reference.
+ * A camera record is 21 float64: R row-major (9; X_cam = R (P - T)), T (3), f (2), c (2),
+ * k (3), p (2) -- the tuple of src/cameras.py:92-140 (load_camera_params / load_cameras).
+ * ------------------------------------------------------------------------------------- */
+
+/* Rigid camera transforms of n points for each of C cameras into out [C, n, 3].
+ * inverse = 0: world -> camera, src/cameras.py:55-72 (world_to_camera_frame; the batched
+ *   form of data_utils.transform_world_to_camera, src/data_utils.py:233-257);
+ * inverse = 1: camera -> world, src/cameras.py:74-90 (camera_to_world_frame).
+ * P is [n, 3] shared by all cameras (in_cam_stride = 0) or [C, n, 3] (in_cam_stride = 3n). */
+int p3d_cam_transform(const double* P, int64_t n, int64_t in_cam_stride, const double* cams,
+                      int32_t C, int32_t inverse, double* out, void* stream);
+
+/* Pinhole projection with radial (k1..k3) and tangential (p1, p2) distortion of n world
+ * points for each of C cameras, src/cameras.py:13-53 (project_point_radial; the batched form
+ * of data_utils.project_to_cameras, src/data_utils.py:339-364).  proj [C, n, 2]; depth,
+ * radial, tan, r2 [C, n] are optional (NULL = not written). */
+int p3d_cam_project(const double* P, int64_t n, const double* cams, int32_t C, double* proj,
+                    double* depth, double* radial, double* tan, double* r2, void* stream);
+
+/* Root-centring, src/data_utils.py:474-494 (postprocess_3d): out = poses - tile(poses[:, :3]),
+ * root [F, 3] = poses[:, :3] (may be NULL).  width = 3 * joints; out must not alias poses. */
+int p3d_root_center(const double* poses, int64_t F, int32_t width, double* out, double* root,
+                    void* stream);
+
+/* src/data_utils.py:260-280 (normalize_data): out [F, U] = (x[:, use] - mean[use]) / std[use]
+ * from x [F, D]; out_dtype P3D_DTYPE_F64, or P3D_DTYPE_F32 (the float64 result rounded, as
+ * feeding it to the model's float32 placeholders does). */
+int p3d_normalize(const double* x, int64_t F, int32_t D, const double* mean, const double* stdv,
+                  const int32_t* dims_to_use, int32_t U, void* out, int32_t out_dtype, void* stream);
+
+/* src/data_utils.py:283-311 (unNormalizeData): scatter xn [F, U] (P3D_DTYPE_F32 or F64; the
+ * reference rounds it to float32) into zeros [F, D], then out = that * std + mean (float64).
+ * D <= 256. */
+int p3d_unnormalize(const void* xn, int32_t in_dtype, int64_t F, int32_t U, const double* mean,
+                    const double* stdv, const int32_t* dims_to_use, int32_t D, double* out,
+                    void* stream);
+
+/* np.mean / np.std (population) over axis 0 of x [F, D], D <= 256 -- the statistics of
+ * src/data_utils.py:210-211 (normalization_stats).  Deterministic two-level column sums;
+ * `work` must hold p3d_moments_workspace(F, D) bytes of device memory. */
+int64_t p3d_moments_workspace(int64_t F, int32_t D);
+int p3d_moments(const double* x, int64_t F, int32_t D, double* mean, double* stdv, void* work,
+                int64_t work_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,171 @@
+"""GPU parity of the H3.6M data pipeline (libp3d p3d_cam_* / p3d_root_center / p3d_normalize /
+p3d_unnormalize / p3d_moments, through the C ABI) against the reference's own outputs
+(tests/golden/reference_goldens_data.npz, reference_goldens.npz) and the oracle
+(oracle/ref_data.py) at full H3.6M sizes."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import cameras  # noqa: E402
+import data_pipeline as dp  # noqa: E402
+import data_utils  # noqa: E402
+from oracle import ref_data  # noqa: E402
+from synth_cameras import synth_cameras, synth_world_poses  # noqa: E402
+
+G = np.load(os.path.join(ROOT, "tests", "golden", "reference_goldens_data.npz"), allow_pickle=False)
+G0 = np.load(os.path.join(ROOT, "tests", "golden", "reference_goldens.npz"), allow_pickle=False)
+
+
+def golden_cams():
+    cams = {}
+    for si, subj in enumerate((9, 11)):
+        for ci in range(4):
+            v = G["cams"][si, ci]
+            cams[(subj, ci + 1)] = (v[:9].reshape(3, 3), v[9:12].reshape(3, 1), v[12:14].reshape(2, 1),
+                                    v[14:16].reshape(2, 1), v[16:19].reshape(3, 1), v[19:21].reshape(2, 1),
+                                    str(G["cam_names"][si, ci]))
+    return cams
+
+
+def keyed(prefix, keyname):
+    out = {}
+    for i, k in enumerate(G[keyname]):
+        s, a, q = str(k).split("|")
+        out[(int(s), a, q)] = G["%s_%d" % (prefix, i)]
+    return out
+
+
+def test_project_point_radial_bit_exact():
+    R, T, f, c, k, p, _ = golden_cams()[(9, 1)]
+    proj, D, radial, tan, r2 = cameras.project_point_radial(G["pp_in"], R, T, f, c, k, p)
+    np.testing.assert_array_equal(proj, G["pp_proj"])
+    np.testing.assert_array_equal(D, G["pp_depth"])
+    np.testing.assert_array_equal(radial, G["pp_radial"])
+    np.testing.assert_array_equal(tan, G["pp_tan"])
+    np.testing.assert_array_equal(r2, G["pp_r2"])
+
+
+def test_camera_frames_bit_exact():
+    R, T, *_ = golden_cams()[(9, 1)]
+    np.testing.assert_array_equal(cameras.world_to_camera_frame(G["pp_in"], R, T), G["w2c_out"])
+    np.testing.assert_array_equal(cameras.camera_to_world_frame(G["w2c_out"], R, T), G["c2w_out"])
+
+
+def test_bad_points_raise_like_reference():
+    R, T, f, c, k, p, _ = golden_cams()[(9, 1)]
+    with pytest.raises(AssertionError):
+        cameras.project_point_radial(np.zeros((4, 2)), R, T, f, c, k, p)
+    with pytest.raises(AssertionError):
+        cameras.world_to_camera_frame(np.zeros(3), R, T)
+    with pytest.raises(ValueError):
+        dp.pack_camera(R, T, f, c, k[:2], p)
+
+
+def test_dict_pipeline_bit_exact():
+    cams = golden_cams()
+    world = keyed("world", "world_keys")
+    cam3d = data_utils.transform_world_to_camera(world, cams)
+    proj2d = data_utils.project_to_cameras(world, cams)
+    g3, g2 = keyed("cam3d", "cam_keys"), keyed("proj2d", "cam_keys")
+    assert list(cam3d) == sorted(g3) and list(proj2d) == sorted(g2)   # the reference's key order
+    for key in g3:
+        np.testing.assert_array_equal(cam3d[key], g3[key])
+        np.testing.assert_array_equal(proj2d[key], g2[key])
+    inp = {k: g3[k].copy() for k in sorted(g3)}
+    centred, roots = data_utils.postprocess_3d(inp)
+    assert centred is inp                                              # in place, like the reference
+    gc, gr = keyed("centred", "cam_keys"), keyed("root", "cam_keys")
+    for key in g3:
+        np.testing.assert_array_equal(centred[key], gc[key])
+        np.testing.assert_array_equal(roots[key], gr[key])
+
+
+def test_normalization_stats_matches_reference():
+    stacked = np.vstack([G["proj2d_%d" % i] for i in range(len(G["cam_keys"]))])
+    mean, std, ign, use = data_utils.normalization_stats(stacked, 2)
+    # a parallel (fixed-order) column sum instead of numpy's sequential one: 1e-13 relative
+    np.testing.assert_allclose(mean, G["ms_mean"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(std, G["ms_std"], rtol=1e-13, atol=0)
+    for d, tag in ((3, "3"), (2, "2")):
+        m, s, i, u = data_utils.normalization_stats(G0["ns_in" + tag], d)
+        np.testing.assert_allclose(m, G0["ns_mean" + tag], rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(s, G0["ns_std" + tag], rtol=1e-13, atol=0)
+        np.testing.assert_array_equal(i, G0["ns_ign" + tag])
+        np.testing.assert_array_equal(u, G0["ns_use" + tag])
+
+
+def test_normalize_and_unnormalize_bit_exact():
+    use = G0["ns_use3"]
+    raw = {(9, "Walking", "a"): G0["nd_in0"].copy(), (11, "Walking", "b"): G0["nd_in1"].copy()}
+    out = data_utils.normalize_data(raw, G0["nd_mean"], G0["nd_std"], use)
+    np.testing.assert_array_equal(out[(9, "Walking", "a")], G0["nd_out0"])
+    np.testing.assert_array_equal(out[(11, "Walking", "b")], G0["nd_out1"])
+    assert raw[(9, "Walking", "a")].shape == (70, 48)                 # the reference's side effect
+    ign = G0["ns_ign3"]
+    np.testing.assert_array_equal(data_utils.unNormalizeData(G0["un_in"], G0["nd_mean"], G0["nd_std"], ign),
+                                  G0["un_out"])
+    np.testing.assert_array_equal(data_utils.unNormalizeData(G0["un_in32"], G0["nd_mean"], G0["nd_std"], ign),
+                                  G0["un_out32"])
+
+
+def test_full_size_pipeline_vs_oracle():
+    """H3.6M-sized subject (two 5000-frame sequences x 4 cameras): transforms bit-identical
+    to the oracle, projections to 1 ulp; moments to 1e-12; normalize -> unnormalize round trip."""
+    rng = np.random.default_rng(5)
+    cams, packed, _ = synth_cameras(rng, subjects=(1,))
+    world = {(1, "Walking", "Walking.h5"): synth_world_poses(rng, 5000),
+             (1, "Walking", "Walking 1.h5"): synth_world_poses(rng, 5000)}
+    p2 = data_utils.project_to_cameras(world, cams)
+    p2o = ref_data.project_to_cameras(world, cams)
+    assert list(p2) == list(p2o)
+    for k in p2o:
+        # r2**3 is numpy's pow, which is not correctly rounded and differs between numpy
+        # versions (the reference's 1.26 and this image's 2.2 disagree on ~28 % of cubes); the
+        # kernel uses the correctly rounded cube: <= 1 ulp through the distortion polynomial
+        np.testing.assert_allclose(p2[k], p2o[k], rtol=4.5e-16, atol=0)
+    c3 = data_utils.transform_world_to_camera(world, cams)
+    c3o = ref_data.transform_world_to_camera(world, cams)
+    for k in c3o:
+        np.testing.assert_array_equal(c3[k], c3o[k])
+    stacked = np.vstack(list(p2o.values()))
+    m, s, _, use = data_utils.normalization_stats(stacked, 2)
+    mo, so = ref_data.moments(stacked)
+    np.testing.assert_allclose(m, mo, rtol=1e-12)
+    np.testing.assert_allclose(s, so, rtol=1e-12)
+    x = dp.normalize(stacked, m, s, use, out_dtype=torch.float32)
+    back = dp.unnormalize(x, m, s, use, 64).cpu().numpy()
+    np.testing.assert_allclose(back[:, use], stacked[:, use], rtol=0, atol=np.abs(stacked).max() * 2e-7)
+
+
+def test_camera_round_trip_and_shared_vs_per_camera_input():
+    rng = np.random.default_rng(6)
+    _, packed, _ = synth_cameras(rng, subjects=(5,))
+    P = rng.normal(0, 500, (1001, 3))                                   # ragged size
+    Xc = dp.world_to_camera(P, packed[0])                              # [4, n, 3]
+    back = dp.camera_to_world(Xc, packed[0]).cpu().numpy()            # per-camera inputs
+    for c in range(4):
+        np.testing.assert_allclose(back[c], P, rtol=0, atol=1e-9)
+    one = dp.camera_to_world(Xc[2], packed[0][2:3]).cpu().numpy()[0]  # shared input form
+    np.testing.assert_array_equal(one, back[2])
+
+
+def test_empty_inputs():
+    rng = np.random.default_rng(7)
+    _, packed, _ = synth_cameras(rng, subjects=(5,))
+    assert dp.project(np.zeros((0, 3)), packed[0]).shape == (4, 0, 2)
+    assert dp.root_center(np.zeros((0, 96)))[0].shape == (0, 96)
+    assert data_utils.normalize_data({}, np.zeros(96), np.ones(96), np.arange(48)) == {}
+    with pytest.raises(ValueError):
+        dp.moments(np.zeros((0, 4)))
