@@ -2233,8 +2233,8 @@ extern "C" int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len) {
 // H3.6M data pipeline (p3d_data.h)
 // =====================================================================================
 static int64_t p3d_moments_blocks(int64_t F) {
-  int64_t g = (F + 511) / 512;
-  return g < 1 ? 1 : (g > 2048 ? 2048 : g);
+  int64_t g = (F + 255) / 256;
+  return g < 1 ? 1 : (g > 4096 ? 4096 : g);
 }
 
 extern "C" int p3d_cam_transform(const double* P, int64_t n, int64_t in_cam_stride, const double* cams,
@@ -2316,7 +2316,7 @@ extern "C" int p3d_moments(const double* x, int64_t F, int32_t D, double* mean, 
   const int64_t G = p3d_moments_blocks(F), chunk = (F + G - 1) / G;
   const hipStream_t st = (hipStream_t)stream;
   double* part = (double*)work;
-  const dim3 gf((unsigned)((D + 255) / 256));
+  const dim3 gf((unsigned)D);
   k_col_partial<1><<<dim3((unsigned)G), 256, 0, st>>>(x, F, D, chunk, nullptr, part);
   k_col_final<1><<<gf, 256, 0, st>>>(part, (int)G, D, F, mean);
   k_col_partial<2><<<dim3((unsigned)G), 256, 0, st>>>(x, F, D, chunk, mean, part);

@@ -146,7 +146,9 @@ __global__ __launch_bounds__(256) void k_unnormalize(const void* __restrict__ xn
 
 // Column sums of a row-major [F, D] float64 matrix in two deterministic levels.
 // Level 1: block b sums rows [b*chunk, (b+1)*chunk) of every column (PASS 1: x, PASS 2:
-// (x - mean)^2), threads = rpb row lanes x D columns, lane partials folded in fixed order.
+// (x - mean)^2); thread = (row lane, column), rpb = 256 / D row lanes; each lane keeps 4
+// independent accumulators (rows r, r+rpb, r+2rpb, r+3rpb of every group of 4 rpb) so four
+// loads are in flight per thread; accumulators and lanes are folded in a fixed order.
 template <int PASS>
 __global__ __launch_bounds__(256) void k_col_partial(const double* __restrict__ x, int64_t F, int D, int64_t chunk,
                                                      const double* __restrict__ mean, double* __restrict__ part) {
@@ -159,11 +161,21 @@ __global__ __launch_bounds__(256) void k_col_partial(const double* __restrict__ 
   double s = 0.0;
   if (lane < rpb) {
     const double mu = PASS == 2 ? mean[d] : 0.0;
-    for (int64_t r = r0 + lane; r < r1; r += rpb) {
-      const double v = x[r * D + d];
-      if (PASS == 1) s += v;
-      else { const double e = v - mu; s += e * e; }
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int64_t r = r0 + lane;
+    const int64_t step = rpb;
+    for (; r + 3 * step < r1; r += 4 * step) {
+      double v0 = x[r * D + d], v1 = x[(r + step) * D + d], v2 = x[(r + 2 * step) * D + d],
+             v3 = x[(r + 3 * step) * D + d];
+      if (PASS == 2) { v0 -= mu; v1 -= mu; v2 -= mu; v3 -= mu; v0 *= v0; v1 *= v1; v2 *= v2; v3 *= v3; }
+      a0 += v0; a1 += v1; a2 += v2; a3 += v3;
     }
+    for (; r < r1; r += step) {
+      double v = x[r * D + d];
+      if (PASS == 2) { v -= mu; v *= v; }
+      a0 += v;
+    }
+    s = (a0 + a1) + (a2 + a3);
   }
   red[t] = s;
   __syncthreads();
@@ -174,15 +186,25 @@ __global__ __launch_bounds__(256) void k_col_partial(const double* __restrict__ 
   }
 }
 
-// Level 2: column d sums the G block partials in order; PASS 1 -> mean, PASS 2 -> std.
+// Level 2: block d folds column d's G block partials (thread t: partials t, t+256, ...;
+// then a fixed LDS tree); PASS 1 -> mean = sum / F, PASS 2 -> std = sqrt(sum / F).
 template <int PASS>
 __global__ __launch_bounds__(256) void k_col_final(const double* __restrict__ part, int G, int D, int64_t F,
                                                    double* __restrict__ out) {
 #pragma clang fp contract(off)
-  const int d = blockIdx.x * 256 + threadIdx.x;
-  if (d >= D) return;
+  __shared__ double red[256];
+  const int d = blockIdx.x, t = threadIdx.x;
   double s = 0.0;
-  for (int g = 0; g < G; ++g) s += part[(int64_t)g * D + d];
-  const double m = s / (double)F;
-  out[d] = PASS == 1 ? m : sqrt(m);
+  for (int g = t; g < G; g += 256) s += part[(int64_t)g * D + d];
+  red[t] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double m = red[0] / (double)F;
+    out[d] = PASS == 1 ? m : sqrt(m);
+  }
 }

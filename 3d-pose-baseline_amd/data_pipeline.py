@@ -67,12 +67,21 @@ def _points(P, what):
     return t
 
 
-def world_to_camera(P, cams):
-    """[n, 3] world points -> [C, n, 3] camera-frame points (one slab per camera)."""
+def _out(out, shape, dev, what):
     torch = _torch()
+    if out is None:
+        return torch.empty(shape, dtype=torch.float64, device=dev)
+    if tuple(out.shape) != tuple(shape) or out.dtype != torch.float64 or not out.is_contiguous() \
+            or out.device != dev:
+        raise ValueError("%s: out must be a contiguous float64 %s tensor on %s" % (what, tuple(shape), dev))
+    return out
+
+
+def world_to_camera(P, cams, out=None):
+    """[n, 3] world points -> [C, n, 3] camera-frame points (one slab per camera)."""
     P = _points(P, "world_to_camera")
     cm = as_device(cams).reshape(-1, CAM_DOUBLES)
-    out = torch.empty((cm.shape[0], P.shape[0], 3), dtype=torch.float64, device=P.device)
+    out = _out(out, (cm.shape[0], P.shape[0], 3), P.device, "world_to_camera")
     check(lib().p3d_cam_transform(ptr(P), P.shape[0], 0, ptr(cm), cm.shape[0], 0, ptr(out), _stream()),
           "p3d_cam_transform")
     return out
@@ -95,13 +104,13 @@ def camera_to_world(X, cams):
     return out
 
 
-def project(P, cams, aux=False):
+def project(P, cams, aux=False, out=None):
     """[n, 3] world points -> projections [C, n, 2]; with aux also depth, radial, tan, r2 [C, n]."""
     torch = _torch()
     P = _points(P, "project")
     cm = as_device(cams).reshape(-1, CAM_DOUBLES)
     C, n = cm.shape[0], P.shape[0]
-    proj = torch.empty((C, n, 2), dtype=torch.float64, device=P.device)
+    proj = _out(out, (C, n, 2), P.device, "project")
     extra = [torch.empty((C, n), dtype=torch.float64, device=P.device) for _ in range(4)] if aux else [None] * 4
     check(lib().p3d_cam_project(ptr(P), n, ptr(cm), C, ptr(proj), *[ptr(e) for e in extra], _stream()),
           "p3d_cam_project")
@@ -120,6 +129,18 @@ def root_center(poses):
     return out, root
 
 
+def _dims(dims, D, what):
+    """Column indices as a device int32 tensor.  Host indices are range-checked here; a device
+    int32 tensor is taken as already checked (no device -> host sync on the hot path)."""
+    torch = _torch()
+    if isinstance(dims, torch.Tensor) and dims.is_cuda and dims.dtype == torch.int32:
+        return dims.reshape(-1).contiguous()
+    d = np.asarray(dims.cpu() if isinstance(dims, torch.Tensor) else dims, np.int64).reshape(-1)
+    if d.size and (d.min() < 0 or d.max() >= D):
+        raise ValueError("%s: dimension indices out of range [0, %d)" % (what, D))
+    return as_device(d.astype(np.int32), torch.int32)
+
+
 def normalize(x, mean, std, dims_to_use, out_dtype=None):
     """(x[:, use] - mean[use]) / std[use]: [F, D] -> [F, U] (float64, or float32)."""
     torch = _torch()
@@ -129,11 +150,9 @@ def normalize(x, mean, std, dims_to_use, out_dtype=None):
         raise ValueError("normalize: expected [F, D], got %s" % (tuple(x.shape),))
     D = x.shape[1]
     mean, std = as_device(mean).reshape(-1), as_device(std).reshape(-1)
-    use = as_device(np.asarray(dims_to_use, np.int64).astype(np.int32), torch.int32).reshape(-1)
+    use = _dims(dims_to_use, D, "normalize")
     if mean.numel() != D or std.numel() != D:
         raise ValueError("normalize: mean/std must have %d entries" % D)
-    if use.numel() and (int(use.min()) < 0 or int(use.max()) >= D):
-        raise ValueError("normalize: dims_to_use out of range [0, %d)" % D)
     out = torch.empty((x.shape[0], use.numel()), dtype=out_dtype, device=x.device)
     code = _p3d.P3D_DTYPE_F32 if out_dtype == torch.float32 else _p3d.P3D_DTYPE_F64
     check(lib().p3d_normalize(ptr(x), x.shape[0], D, ptr(mean), ptr(std), ptr(use), use.numel(), ptr(out), code,
@@ -152,7 +171,7 @@ def unnormalize(xn, mean, std, dims_to_use, D=None):
         raise ValueError("unnormalize: expected [F, U], got %s" % (tuple(t.shape),))
     mean, std = as_device(mean).reshape(-1), as_device(std).reshape(-1)
     D = D or mean.numel()
-    use = as_device(np.asarray(dims_to_use, np.int64).astype(np.int32), torch.int32).reshape(-1)
+    use = _dims(dims_to_use, D, "unnormalize")
     if use.numel() != t.shape[1]:
         raise ValueError("unnormalize: %d columns for %d used dimensions" % (t.shape[1], use.numel()))
     out = torch.empty((t.shape[0], D), dtype=torch.float64, device=t.device)

@@ -550,12 +550,132 @@ def bench_stress(args, rank, world):
     return value, dt, roof, steps
 
 
+def bench_data(args, rank, world):
+    """The H3.6M training-set preprocessing of create_2d_data / read_3d_data
+    (src/data_utils.py:395-471) on the GPU: world poses of 5 subjects x 150 sequences
+    (390,000 frames, H3.6M's train-set size) -> 2D projections into 4 cameras, their
+    mean/std and normalisation; camera-frame 3D, root-centring, mean/std, normalisation.
+    Float64 like the reference, inputs resident in HBM; every rank runs the whole set
+    (replicas)."""
+    import torch
+    import data_pipeline as dp
+    import data_utils
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from synth_cameras import synth_cameras, synth_world_poses
+    rng = np.random.default_rng(77)
+    subjects = (1, 5, 6, 7, 8)
+    frames = args.data_frames // len(subjects)
+    cams, packed, _ = synth_cameras(rng, subjects)
+    W = [dp.as_device(synth_world_poses(rng, frames)).reshape(-1, 3) for _ in subjects]
+    C = [dp.as_device(packed[i]) for i in range(len(subjects))]
+    use2 = torch.from_numpy(data_utils.dimension_sets(2)[0].astype(np.int32)).cuda()
+    use3 = torch.from_numpy(data_utils.dimension_sets(3)[0].astype(np.int32)).cuda()
+    S, n = len(subjects), frames * 32
+    p2 = torch.empty((S, 4, n, 2), dtype=torch.float64, device="cuda")
+    c3 = torch.empty((S, 4, n, 3), dtype=torch.float64, device="cuda")
+    ev = {}
+
+    def mark(tag):
+        if ev is not None and tag in ev:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev[tag].append(e)
+
+    def step():
+        mark("project0")
+        for i in range(S):
+            dp.project(W[i], C[i], out=p2[i])
+        mark("project1")
+        x2 = p2.reshape(-1, 64)
+        m2, s2 = dp.moments(x2)
+        mark("normalize2_0")
+        n2 = dp.normalize(x2, m2, s2, use2)
+        mark("normalize2_1")
+        mark("transform0")
+        for i in range(S):
+            dp.world_to_camera(W[i], C[i], out=c3[i])
+        mark("transform1")
+        cen, root = dp.root_center(c3.reshape(-1, 96))
+        mark("moments3_0")
+        m3, s3 = dp.moments(cen)
+        mark("moments3_1")
+        n3 = dp.normalize(cen, m3, s3, use3)
+        return n2, n3
+
+    ev = None
+    step()
+    torch.cuda.synchronize()
+    reps = args.data_reps
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world) / reps
+    # stage timing (one instrumented pass): which kernel dominates
+    ev = {k: [] for k in ("project0", "project1", "normalize2_0", "normalize2_1", "transform0", "transform1",
+                          "moments3_0", "moments3_1")}
+    step()
+    torch.cuda.synchronize()
+    ms = lambda a, b: ev[a][0].elapsed_time(ev[b][0])   # noqa: E731
+    F2 = S * 4 * frames
+    stages = {
+        # algorithmic bytes: inputs read once, outputs written once
+        "k_cam_points<2> (project, 5 launches)": (ms("project0", "project1"), S * (n * 24 + 4 * n * 16)),
+        "k_cam_points<0> (world->camera, 5 launches)": (ms("transform0", "transform1"), S * (n * 24 + 4 * n * 24)),
+        "k_col_partial x2 + k_col_final x2 (moments 3D)": (ms("moments3_0", "moments3_1"), 2 * F2 * 96 * 8),
+        "k_normalize (2D)": (ms("normalize2_0", "normalize2_1"), F2 * 64 * 8 + F2 * 32 * 8),
+    }
+    name, (t_ms, nbytes) = max(stages.items(), key=lambda kv: kv[1][0])
+    ach = nbytes / (t_ms * 1e-3) / 1e9
+    out = {"workload": "H3.6M train-set preprocessing (create_2d_data + read_3d_data numerics), "
+                       "%d world frames x 4 cameras, float64" % (S * frames),
+           "value": round(F2 / dt, 1), "unit": "camera-poses/s", "ms_per_pass": round(1000.0 * dt, 3),
+           "reps": reps,
+           "stages_ms": {k: round(v[0], 4) for k, v in stages.items()},
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(ach / 8000.0, 4), "traffic": None, "kernel": name,
+                        "bytes_per_pass": int(nbytes), "avg_us": round(1000.0 * t_ms, 2),
+                        "stages_ms": {k: round(v[0], 4) for k, v in stages.items()}}}
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_data_baseline(args.cpu_seconds / 2)
+    return out
+
+
+def cpu_data_baseline(seconds):
+    """The oracle's numpy pipeline (oracle/ref_data.py) on sequences of one subject, as many
+    as fit in ~seconds: camera-poses/s, one host core (numpy is single-threaded here)."""
+    from oracle import ref_data
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from synth_cameras import synth_cameras, synth_world_poses
+    rng = np.random.default_rng(78)
+    cams, _, _ = synth_cameras(rng, (1,))
+    seq = {(1, "Walking", "Walking %d.h5" % i): synth_world_poses(rng, 2600) for i in range(4)}
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        p2 = ref_data.project_to_cameras(seq, cams)
+        x2 = np.vstack(list(p2.values()))
+        m2, s2 = ref_data.moments(x2)
+        use2 = np.flatnonzero(s2 > 0)
+        _ = (x2[:, use2] - m2[use2]) / s2[use2]
+        c3 = ref_data.transform_world_to_camera(seq, cams)
+        cen, _ = ref_data.postprocess_3d(c3)
+        x3 = np.vstack(list(cen.values()))
+        m3, s3 = ref_data.moments(x3)
+        use3 = np.flatnonzero(s3 > 0)
+        _ = (x3[:, use3] - m3[use3]) / s3[use3]
+        done += x2.shape[0]
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 1), "unit": "camera-poses/s", "cores": 1, "kind": "port",
+            "sample": "%d camera-poses (4 sequences x 2600 frames x 4 cameras per pass), %.1f s" % (done, dt)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--mode", choices=["infer", "train", "eval", "stress"], default="infer")
+    ap.add_argument("--mode", choices=["infer", "train", "eval", "stress", "data"], default="infer")
     ap.add_argument("--graph-steps", type=int, default=240)
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--queue-probe", type=int, default=0,
@@ -570,13 +690,16 @@ def main():
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
     ap.add_argument("--no-api", action="store_true", help="skip the LinearModel.step() API-level rates (infer mode)")
     ap.add_argument("--procrustes", action="store_true", help="cfg4 sweep with Protocol #2 alignment")
+    ap.add_argument("--no-data", action="store_true", help="skip the H3.6M preprocessing sub-measurement")
+    ap.add_argument("--data-frames", type=int, default=390000)
+    ap.add_argument("--data-reps", type=int, default=10)
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
     rank, world, local = setup_dist()
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    train = single = sweep = api = None
+    train = single = sweep = api = data = None
     if args.mode == "infer":
         value, dt, roof, single = bench_infer(args, rank, world)
         workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
@@ -600,11 +723,22 @@ def main():
                 api = bench_api(args, rank, world)
             except Exception as exc:
                 api = {"error": repr(exc)[:300]}
+        if not args.no_data:
+            try:
+                data = bench_data(args, rank, world)
+            except Exception as exc:
+                data = {"error": repr(exc)[:300]}
     elif args.mode == "eval":
         sweep = bench_eval(args, rank, world)
         value, dt, roof = sweep["value"], sweep["ms_per_sweep"] / 1000.0, sweep.pop("roofline")
         args.steps = 1
         workload = sweep["workload"]
+    elif args.mode == "data":
+        data = bench_data(args, rank, world)
+        value, roof = data["value"], data.pop("roofline")
+        args.steps = data["reps"]
+        dt = data["ms_per_pass"] / 1000.0 * args.steps
+        workload = data["workload"]
     elif args.mode == "stress":
         value, dt, roof, args.steps = bench_stress(args, rank, world)
         workload = "cfg5 inference: L=4096, 4 residual blocks, BN(eval), batch 1024 per step, bf16/fp32-acc"
@@ -613,16 +747,22 @@ def main():
         workload = ("cfg3 train step: L=1024, 2 residual blocks, BN, dropout keep 0.5, batch 64/GPU, TF1 Adam "
                     "(%s)" % tmode)
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(args.mode, args.cpu_seconds)
-        if args.mode == "stress":
+        if args.mode == "data":
+            cpu = data.pop("cpu_baseline", None)
+        elif args.mode == "stress" or args.no_cpu:
             cpu = None
+        else:
+            cpu = cpu_baseline(args.mode, args.cpu_seconds)
         metric = {"stress": "poses/sec at batch 1024 (cfg5 bf16 stress)",
-                  "eval": "frames/sec, evaluateActionWise MPJPE sweep (cfg4)"}.get(
+                  "eval": "frames/sec, evaluateActionWise MPJPE sweep (cfg4)",
+                  "data": "camera-poses/sec, H3.6M train-set preprocessing (float64)"}.get(
                       args.mode, "poses/sec at batch 64 (H3.6M 16-joint)")
-        line = {"metric": metric, "value": round(value, 1), "unit": "frames/s" if args.mode == "eval" else "poses/s",
+        unit = {"eval": "frames/s", "data": "camera-poses/s"}.get(args.mode, "poses/s")
+        line = {"metric": metric, "value": round(value, 1), "unit": unit,
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(1000.0 * dt / args.steps, 5), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.mode == "stress" else "f32",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": {"stress": "bf16", "data": "f64"}.get(args.mode, "f32"),
                 "data": "synthetic",
                 "config": ({"workload": workload, "global_batch": BATCH * world, "linear_size": L,
                             "num_layers": NBLK, "parallelism": "dp%d" % world} if args.mode != "stress" else
@@ -637,6 +777,8 @@ def main():
             line["eval_sweep"] = sweep
         if api is not None:
             line["api_step"] = api
+        if data is not None and args.mode != "data":
+            line["data_pipeline"] = data
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
