@@ -228,6 +228,7 @@ class LinearModel(object):
 
         self._loss_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._step_host = 0   # host mirror of the device global_step (step() summaries, no sync)
+        self._host_steps = {}  # step() staging buffers / eval graphs per (mode, B, keep)
         self._dy = torch.empty((self.max_batch, self.output_size), dtype=torch.float32, device=self.device)
         if init:
             self.initialize(self.seed)
@@ -472,6 +473,9 @@ class LinearModel(object):
         """
         torch = self.torch
         with torch.cuda.device(self.device):
+            if not isinstance(encoder_inputs, torch.Tensor) and not isinstance(decoder_outputs, torch.Tensor):
+                return self._step_host_arrays(encoder_inputs, decoder_outputs, float(dropout_keep_prob),
+                                              bool(isTraining))
             if isTraining:
                 lr = exponential_decay(self.lr0, self._step_host)   # lr of this step (gs before the update)
                 loss, y = self.train_step_device(encoder_inputs, decoder_outputs, dropout_keep_prob)
@@ -486,6 +490,80 @@ class LinearModel(object):
             lv = float(loss.item())
             return lv, Summary("loss/loss", lv), out
 
+    # ---- step() from host arrays: the session.run path with one H2D, one D2H, one sync ------
+    def _host_step_state(self, training, B, keep):
+        """Pinned staging buffers (and, for evaluation, a HIP graph of H2D copy + forward +
+        MSE + D2H copy) for one (mode, batch, keep_prob), cached."""
+        torch = self.torch
+        key = (training, B, keep, self.lr0, self.seed)
+        st = self._host_steps.get(key)
+        if st is not None:
+            return st
+        while len(self._host_steps) >= 8:
+            self._host_steps.pop(next(iter(self._host_steps)))
+        f32 = torch.float32
+        st = {"hx": torch.empty((B, self.input_size), dtype=f32, pin_memory=True),
+              "ht": torch.empty((B, self.output_size), dtype=f32, pin_memory=True),
+              "hy": torch.empty((B, self.output_size), dtype=f32, pin_memory=True),
+              "hl": torch.empty(1, dtype=f32, pin_memory=True),
+              "dx": torch.empty((B, self.input_size), dtype=f32, device=self.device),
+              "dt": torch.empty((B, self.output_size), dtype=f32, device=self.device),
+              "dy": torch.empty((B, self.output_size), dtype=f32, device=self.device),
+              "graph": None}
+        st["hx_np"], st["ht_np"] = st["hx"].numpy(), st["ht"].numpy()
+        st["hy_np"], st["hl_np"] = st["hy"].numpy(), st["hl"].numpy()
+        if not training:
+            def body():
+                st["dx"].copy_(st["hx"], non_blocking=True)
+                st["dt"].copy_(st["ht"], non_blocking=True)
+                self.forward_device(st["dx"], False, keep, out=st["dy"])
+                loss = self.loss_device(st["dy"], st["dt"])
+                st["hy"].copy_(st["dy"], non_blocking=True)
+                st["hl"].copy_(loss, non_blocking=True)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                body()                      # eager warm-up (evaluation has no side effects)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                body()
+            st["graph"] = g
+        self._host_steps[key] = st
+        return st
+
+    def _step_host_arrays(self, encoder_inputs, decoder_outputs, keep, training):
+        x = np.asarray(encoder_inputs)
+        t = np.asarray(decoder_outputs)
+        if x.ndim != 2 or x.shape[1] != self.input_size:
+            raise ValueError("enc_in: expected shape [None, %d], got %s" % (self.input_size, x.shape))
+        if t.ndim != 2 or t.shape[1] != self.output_size:
+            raise ValueError("dec_out: expected shape [None, %d], got %s" % (self.output_size, t.shape))
+        if t.shape[0] != x.shape[0]:
+            raise ValueError("enc_in has %d rows, dec_out %d" % (x.shape[0], t.shape[0]))
+        B = x.shape[0]
+        if B > self.max_batch:
+            raise ValueError("batch %d exceeds max_batch %d" % (B, self.max_batch))
+        st = self._host_step_state(training, B, keep)
+        np.copyto(st["hx_np"], x, casting="unsafe")     # float64 -> float32, as the placeholders cast
+        np.copyto(st["ht_np"], t, casting="unsafe")
+        stream = self.torch.cuda.current_stream(self.device)
+        if st["graph"] is not None:
+            st["graph"].replay()
+        else:
+            lr = exponential_decay(self.lr0, self._step_host)
+            st["dx"].copy_(st["hx"], non_blocking=True)
+            st["dt"].copy_(st["ht"], non_blocking=True)
+            loss, _ = self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"])
+            st["hy"].copy_(st["dy"], non_blocking=True)
+            st["hl"].copy_(loss, non_blocking=True)
+        stream.synchronize()
+        lv = float(st["hl_np"][0])
+        out = st["hy_np"].copy()
+        if training:
+            return lv, Summary("loss/loss", lv), Summary("learning_rate/learning_rate", lr), out
+        return lv, Summary("loss/loss", lv), out
+
     def get_all_batches(self, data_x, data_y, camera_frame, training=True):
         """src/linear_model.py:247-300 (see ``get_all_batches`` below)."""
         return get_all_batches(data_x, data_y, camera_frame, self.batch_size, self.input_size,
@@ -494,6 +572,7 @@ class LinearModel(object):
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self.torch.cuda.synchronize(self.device)
+            self._host_steps.clear()   # graphs over the model's buffers go first
             lib().p3d_destroy(self._h)
             self._h = _p3d.c_void_p()
 

@@ -486,6 +486,17 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
         barrier_sync(world)
         dt = max_over_ranks(time.perf_counter() - t0, world)
         out[name] = {"value": round(world * n * BATCH / dt, 1), "unit": "poses/s", "ms_per_step": round(1000.0 * dt / n, 4)}
+    # the OpenPose front end's per-frame call (src/openpose_3dpose_sandbox.py:317-356): B = 1
+    x1, t1 = xs[0][:1], np.zeros((1, OUT))
+    for i in range(20):
+        model.step(None, x1, t1, 1.0, isTraining=False)
+    t0 = time.perf_counter()
+    n1 = 2 * n_infer
+    for i in range(n1):
+        model.step(None, x1, t1, 1.0, isTraining=False)
+    dt = time.perf_counter() - t0
+    out["eval_b1"] = {"us_per_call": round(1e6 * dt / n1, 2), "unit": "us",
+                      "note": "LinearModel.step() at batch 1 from numpy: H2D, 6 layer kernels, MSE, D2H, sync"}
     model.close()
     return out
 
