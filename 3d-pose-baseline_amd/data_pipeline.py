@@ -141,7 +141,7 @@ def _dims(dims, D, what):
     return as_device(d.astype(np.int32), torch.int32)
 
 
-def normalize(x, mean, std, dims_to_use, out_dtype=None):
+def normalize(x, mean, std, dims_to_use, out_dtype=None, out=None):
     """(x[:, use] - mean[use]) / std[use]: [F, D] -> [F, U] (float64, or float32)."""
     torch = _torch()
     out_dtype = out_dtype or torch.float64
@@ -153,14 +153,18 @@ def normalize(x, mean, std, dims_to_use, out_dtype=None):
     use = _dims(dims_to_use, D, "normalize")
     if mean.numel() != D or std.numel() != D:
         raise ValueError("normalize: mean/std must have %d entries" % D)
-    out = torch.empty((x.shape[0], use.numel()), dtype=out_dtype, device=x.device)
+    if out is None:
+        out = torch.empty((x.shape[0], use.numel()), dtype=out_dtype, device=x.device)
+    elif tuple(out.shape) != (x.shape[0], use.numel()) or out.dtype != out_dtype or not out.is_contiguous():
+        raise ValueError("normalize: out must be a contiguous %s [%d, %d] tensor"
+                         % (out_dtype, x.shape[0], use.numel()))
     code = _p3d.P3D_DTYPE_F32 if out_dtype == torch.float32 else _p3d.P3D_DTYPE_F64
     check(lib().p3d_normalize(ptr(x), x.shape[0], D, ptr(mean), ptr(std), ptr(use), use.numel(), ptr(out), code,
                               _stream()), "p3d_normalize")
     return out
 
 
-def unnormalize(xn, mean, std, dims_to_use, D=None):
+def unnormalize(xn, mean, std, dims_to_use, D=None, out=None):
     """Inverse of normalize as unNormalizeData computes it: [F, U] -> [F, D] float64."""
     torch = _torch()
     t = xn if isinstance(xn, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(xn))
@@ -174,7 +178,7 @@ def unnormalize(xn, mean, std, dims_to_use, D=None):
     use = _dims(dims_to_use, D, "unnormalize")
     if use.numel() != t.shape[1]:
         raise ValueError("unnormalize: %d columns for %d used dimensions" % (t.shape[1], use.numel()))
-    out = torch.empty((t.shape[0], D), dtype=torch.float64, device=t.device)
+    out = _out(out, (t.shape[0], D), t.device, "unnormalize")
     code = _p3d.P3D_DTYPE_F32 if t.dtype == torch.float32 else _p3d.P3D_DTYPE_F64
     check(lib().p3d_unnormalize(ptr(t), code, t.shape[0], use.numel(), ptr(mean), ptr(std), ptr(use), D, ptr(out),
                                 _stream()), "p3d_unnormalize")

@@ -497,6 +497,26 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
     dt = time.perf_counter() - t0
     out["eval_b1"] = {"us_per_call": round(1e6 * dt / n1, 2), "unit": "us",
                       "note": "LinearModel.step() at batch 1 from numpy: H2D, 6 layer kernels, MSE, D2H, sync"}
+    # the front end's whole per-frame path as one graph (openpose_frontend.FrameLifter):
+    # pinned H2D of the mapped frame, normalise, 6 layers, unNormalizeData, D2H
+    import data_utils
+    import openpose_frontend
+    rng2 = np.random.default_rng(600)
+    use2, _ = data_utils.dimension_sets(2)
+    _, ign3 = data_utils.dimension_sets(3)
+    fl = openpose_frontend.FrameLifter(model, rng2.uniform(200, 600, 64), rng2.uniform(50, 150, 64), use2,
+                                       rng2.uniform(-400, 400, 96), rng2.uniform(30, 300, 96), ign3, batch=1)
+    e = openpose_frontend.map_frames(rng2.uniform(100, 900, (1, 36)))
+    for i in range(20):
+        fl.lift_mapped(e)
+    t0 = time.perf_counter()
+    for i in range(n1):
+        fl.lift_mapped(e)
+    dt = time.perf_counter() - t0
+    out["frontend_b1"] = {"us_per_frame": round(1e6 * dt / n1, 2), "unit": "us",
+                          "note": "openpose_frontend.FrameLifter: one HIP graph per frame (normalise, "
+                                  "6 layers, unNormalizeData) + pinned H2D/D2H + sync"}
+    del fl
     model.close()
     return out
 

@@ -168,3 +168,15 @@ def test_checkpoint_io_names_and_order():
     assert f == "0007 - linear_model-batch_normalization-gamma:0.npy"
     assert cio.parse_dump_filename(f) == (7, "linear_model/batch_normalization/gamma")
     assert cio.parse_dump_filename("notes.txt") is None
+
+
+def test_openpose_mapping_matches_oracle():
+    """Host joint mapping of the OpenPose front end (src/openpose_3dpose_sandbox.py:25,326-342)."""
+    import openpose_frontend
+    from oracle import ref_frontend
+    rng = np.random.default_rng(9)
+    frames = rng.uniform(0, 1000, (7, 36))
+    got = openpose_frontend.map_frames(frames)
+    for i in range(7):
+        np.testing.assert_array_equal(got[i], ref_frontend.map_frame(frames[i]))
+    assert openpose_frontend.ORDER == ref_frontend.ORDER

@@ -1,0 +1,64 @@
+"""OpenPose front-end lifting: FrameLifter's one-graph-per-frame path
+(H2D, p3d_normalize, the six layer kernels, p3d_unnormalize, D2H) against the oracle's
+per-frame restatement of src/openpose_3dpose_sandbox.py:317-356."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import data_utils  # noqa: E402
+import linear_model  # noqa: E402
+import openpose_frontend as of  # noqa: E402
+from oracle import ref_frontend, ref_mlp  # noqa: E402
+
+
+def setup(seed=3):
+    rng = np.random.default_rng(seed)
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=seed, bn_seed=seed + 1)
+    m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_fe", seed=11)
+    m.set_weights({**st.params, **st.moving})
+    use2, _ = data_utils.dimension_sets(2)
+    use3, ign3 = data_utils.dimension_sets(3)
+    stats = dict(mean2=rng.uniform(200, 600, 64), std2=rng.uniform(50, 150, 64),
+                 mean3=rng.uniform(-400, 400, 96), std3=rng.uniform(30, 300, 96))
+    frames = rng.uniform(100, 900, (23, 36))      # 23 OpenPose frames, 18 joints x (x, y)
+    return st, m, stats, use2, use3, ign3, frames
+
+
+def test_frame_lifter_matches_oracle_and_batches_agree():
+    st, m, s, use2, use3, ign3, frames = setup()
+    fl1 = of.FrameLifter(m, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3, batch=1)
+    got = fl1.lift(frames)
+    ref_mm, ref_norm = ref_frontend.lift_frames(st, frames, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3)
+    # network outputs vs the fp64 oracle (the tolerance of the MLP parity tests), then x std
+    norm = (got[:, use3] - s["mean3"][use3]) / s["std3"][use3]
+    err = np.abs(norm - ref_norm)
+    assert np.all(err <= 2e-5 + 2e-5 * np.abs(ref_norm)), err.max()
+    np.testing.assert_array_equal(got[:, ign3], np.tile(s["mean3"][ign3], (len(frames), 1)))
+    assert np.abs(got - ref_mm).max() <= 1e-4 * s["std3"].max()
+    fl8 = of.FrameLifter(m, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3, batch=8)
+    np.testing.assert_array_equal(fl8.lift(frames), got)      # 3 calls, ragged last one
+    m.close()
+
+
+def test_frame_lifter_rejects_bad_input():
+    st, m, s, use2, use3, ign3, frames = setup(4)
+    fl = of.FrameLifter(m, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3, batch=2)
+    with pytest.raises(ValueError):
+        fl.lift_mapped(np.zeros((3, 64)))
+    with pytest.raises(ValueError):
+        of.map_frames(np.zeros((2, 10)))
+    with pytest.raises(ValueError):
+        of.FrameLifter(m, s["mean2"], s["std2"], use2[:10], s["mean3"], s["std3"], ign3)
+    m.close()
