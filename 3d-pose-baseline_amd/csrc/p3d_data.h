@@ -182,11 +182,12 @@ __global__ __launch_bounds__(256) void k_col_partial(const double* __restrict__ 
   if (t < D) {
     double acc = red[t];
     for (int l = 1; l < rpb; ++l) acc += red[l * D + t];
-    part[(int64_t)blockIdx.x * D + t] = acc;
+    part[(int64_t)t * gridDim.x + blockIdx.x] = acc;   // column-major: the fold reads rows
   }
 }
 
-// Level 2: block d folds column d's G block partials (thread t: partials t, t+256, ...;
+// Level 2: block d folds column d's G block partials (part[d][g], contiguous; thread t:
+// partials t, t+256, ...;
 // then a fixed LDS tree); PASS 1 -> mean = sum / F, PASS 2 -> std = sqrt(sum / F).
 template <int PASS>
 __global__ __launch_bounds__(256) void k_col_final(const double* __restrict__ part, int G, int D, int64_t F,
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(256) void k_col_final(const double* __restrict__ pa
   __shared__ double red[256];
   const int d = blockIdx.x, t = threadIdx.x;
   double s = 0.0;
-  for (int g = t; g < G; g += 256) s += part[(int64_t)g * D + d];
+  for (int g = t; g < G; g += 256) s += part[(int64_t)d * G + g];
   red[t] = s;
   __syncthreads();
 #pragma unroll
