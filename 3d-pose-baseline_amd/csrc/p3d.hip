@@ -1528,6 +1528,8 @@ static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch
     const int gy = (a.M + 15) / 16, gy2 = (a.M + 31) / 32;
     if (wk == 8) go(ps, k_fwd<1, 8, 8, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
     else if (wk == 84) go(ps, k_fwd<1, 8, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 85) go(ps, k_fwd<1, 8, 3, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
+    else if (wk == 86) go(ps, k_fwd<1, 8, 3, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
     else if (wk == 82) go(ps, k_fwd<1, 8, 2, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
     else if (wk == 80) go(ps, k_fwd<1, 8, 1, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
     else if (wk == 83) go(ps, k_fwd<1, 8, 2, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
@@ -1769,6 +1771,9 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
       m->nlossp = (int)(((ly.N + 15) / 16) * ((B + 15) / 16));
     }
     const int kind = (l == 0) ? 0 : (last ? 2 : 1);
+#ifdef P3D_DIAG_SKIP_IN   // diagnostic builds only (tools/): drop the input-layer launch
+    if (!training && l == 0) { in = a.Y; continue; }
+#endif
     if (training && ly.bn && m->train_split) {
       const int rc = launch_fwd_split(m, a, kind, st);
       if (rc) return rc;
@@ -2123,6 +2128,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     switch (m->infer_wk) {
       case 8: n = "k_fwd<1, 8, 8, 2, true, true, 1>"; break;
       case 84: n = "k_fwd<1, 8, 4, 2, true, true, 1>"; break;
+      case 85: n = "k_fwd<1, 8, 3, 2, true, true, 1>"; break;
+      case 86: n = "k_fwd<1, 8, 3, 1, true, true, 1>"; break;
       case 82: n = "k_fwd<1, 8, 2, 2, true, true, 1>"; break;
       case 80: n = "k_fwd<1, 8, 1, 2, true, true, 1>"; break;
       case 83: n = "k_fwd<1, 8, 2, 1, true, true, 1>"; break;

@@ -129,6 +129,7 @@ class Saver:
 
     def save(self, session, save_path, global_step=None):
         path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+        self.model.sync_moving_stats()   # data parallel: one set of moving statistics
         state = self.model.get_state()
         d = os.path.dirname(path)
         if d:
@@ -372,6 +373,13 @@ class LinearModel(object):
             check(lib().p3d_set_step(self._h, int(st["global_step"]), float(st["beta1_power"]),
                                      float(st["beta2_power"])), "p3d_set_step")
             self._step_host = int(st["global_step"])
+
+    def sync_moving_stats(self):
+        """Data parallel: average the BN moving statistics over the replicas (each replica's
+        are the EMA of its own 64-row batches; no SyncBN).  Done before each
+        evaluation and checkpoint; a no-op on one GPU."""
+        if self.data_parallel:
+            dist_utils.allreduce_mean_(self.flat["moving"])
 
     def broadcast_parameters(self):
         """Rank 0's variables to every rank (start of data-parallel training)."""

@@ -375,6 +375,7 @@ def train(flags=None):
                   "Learning rate:       %.2e\n"
                   "Train loss avg:      %.4f\n"
                   "=============================" % (model.global_step.eval(), model.learning_rate.eval(), loss))
+            model.sync_moving_stats()   # data parallel: evaluate with the replicas' mean statistics
             if flags.evaluateActionWise:
                 print("{0:=^12} {1:=^6}".format("Action", "mm"))
                 errs, avg = evaluate_action_wise(model, d["test_set_2d"], d["test_set_3d"], d["data_mean_3d"],

@@ -180,9 +180,22 @@ def cpu_baseline(mode, seconds=12.0):
         fn()
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * BATCH / dt, 1), "unit": "poses/s", "cores": int(threads), "kind": "port",
-            "sample": "%d %s batches of 64 (cfg2 model, fp32 numpy restatement of src/linear_model.py), %.1f s"
-                      % (n, "train-step" if mode == "train" else "inference", dt)}
+    out = {"value": round(n * BATCH / dt, 1), "unit": "poses/s", "cores": int(threads), "kind": "port",
+           "sample": "%d %s batches of 64 (cfg2 model, fp32 numpy restatement of src/linear_model.py), %.1f s"
+                     % (n, "train-step" if mode == "train" else "inference", dt)}
+    try:   # the same restatement on one core (SURVEY 8d asks for both)
+        from threadpoolctl import threadpool_limits
+        with threadpool_limits(limits=1):
+            n1, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds / 3:
+                fn()
+                n1 += 1
+            dt1 = time.perf_counter() - t0
+        out["one_core"] = {"value": round(n1 * BATCH / dt1, 1), "unit": "poses/s", "cores": 1,
+                           "sample": "%d batches, %.1f s" % (n1, dt1)}
+    except Exception as exc:
+        out["one_core"] = {"error": repr(exc)[:200]}
+    return out
 
 
 def distinct_queue_streams(n, pool=16, cycles=200_000):

@@ -50,13 +50,22 @@ def _worker(rank, world, port, out):
     flat = m.flat["params"].double().cpu()
     g = [torch.zeros_like(flat) for _ in range(world)]
     dist.all_gather(g, flat)
+    # BN moving statistics: per replica while training, averaged by sync_moving_stats
+    mv = m.flat["moving"].double().cpu()
+    gm = [torch.zeros_like(mv) for _ in range(world)]
+    dist.all_gather(gm, mv)
+    m.sync_moving_stats()
+    mv2 = m.flat["moving"].double().cpu()
+    gm2 = [torch.zeros_like(mv2) for _ in range(world)]
+    dist.all_gather(gm2, mv2)
     # sharded action-wise eval == one process over everything (tables summed over ranks)
     stats = ref_eval.synthetic_stats()
     s2, s3 = ref_eval.synthetic_test_set(scale=0.01)
     acts = ref_eval.define_actions("All")
     errs, avg = predict_3dpose.evaluate_action_wise(m, s2, s3, stats["mean3"], stats["std3"], stats["use3"], acts)
     if rank == 0:
-        np.savez(out, params=torch.stack(g).numpy(), avg=avg, xs=np.stack(xs), ts=np.stack(ts))
+        np.savez(out, params=torch.stack(g).numpy(), avg=avg, xs=np.stack(xs), ts=np.stack(ts),
+                 moving=torch.stack(gm).numpy(), moving_synced=torch.stack(gm2).numpy())
     dist.destroy_process_group()
 
 
@@ -66,3 +75,6 @@ def test_dp_two_ranks_one_gpu(tmp_path):
     r = np.load(out)
     np.testing.assert_array_equal(r["params"][0], r["params"][1])
     assert np.isfinite(r["avg"])
+    assert not np.array_equal(r["moving"][0], r["moving"][1])          # different local batches
+    np.testing.assert_array_equal(r["moving_synced"][0], r["moving_synced"][1])
+    np.testing.assert_allclose(r["moving_synced"][0], r["moving"].mean(axis=0), rtol=1e-6, atol=1e-7)
