@@ -453,8 +453,8 @@ struct BnFwdArgs {
   float* Y;                            // packed [M, N]
 };
 
-// The <= 4 row-tile partial pairs of columns n0..n0+3 ([t][col][2] layout: 8 consecutive
-// floats per tile), all issued up front.
+// The first <= 4 row-tile partial pairs of columns n0..n0+3 ([t][col][2] layout: 8
+// consecutive floats per tile), all issued up front (tiles 4.. of B > 64 are read in the fold).
 __device__ __forceinline__ void p3d_load_parts(const float* part, int M, int N, int n0, f32x4 (&pp)[4][2]) {
   const int R = (M + 15) >> 4;
 #pragma unroll
@@ -501,6 +501,7 @@ __global__ __launch_bounds__(64) void k_bn_fwd(BnFwdArgs p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (t < R) S += pp[t][e >> 1][(e & 1) * 2];
+    for (int t = 4; t < R; ++t) S += p.part[((int64_t)t * p.N + n0 + e) * 2];   // B > 64
     const float mean = S / fm;
     float M2 = 0.f;
 #pragma unroll
@@ -510,6 +511,12 @@ __global__ __launch_bounds__(64) void k_bn_fwd(BnFwdArgs p) {
         const float d = pp[t][e >> 1][(e & 1) * 2] / (float)nt - mean;
         M2 += pp[t][e >> 1][(e & 1) * 2 + 1] + (float)nt * d * d;
       }
+    for (int t = 4; t < R; ++t) {
+      const int nt = min(16, p.M - 16 * t);
+      const float* pt = p.part + ((int64_t)t * p.N + n0 + e) * 2;
+      const float d = pt[0] / (float)nt - mean;
+      M2 += pt[1] + (float)nt * d * d;
+    }
     const float var = M2 / fm;
     mean4[e] = mean;
     var4[e] = var;
@@ -712,6 +719,11 @@ __global__ __launch_bounds__(64) void k_bn_bwd(BnBwdArgs p) {
         sg += pp[t][e >> 1][(e & 1) * 2];
         sgx += pp[t][e >> 1][(e & 1) * 2 + 1];
       }
+    for (int t = 4; t < R; ++t) {   // B > 64
+      const float* pt = p.part + ((int64_t)t * p.K + n0 + e) * 2;
+      sg += pt[0];
+      sgx += pt[1];
+    }
     sg4[e] = sg;
     sgx4[e] = sgx;
     const float rstd = 1.0f / sqrtf(va4[e] + p.eps);
@@ -1124,7 +1136,7 @@ struct p3d_model {
   float* ws = nullptr;        // activation workspace
   float* scratch = nullptr;   // reductions (max-norm)
   float* bnpart = nullptr;    // inside scratch: split BN-train row-tile partials
-  float* lossp = nullptr;     // inside scratch: fused-MSE per-workgroup loss partials (<= 64)
+  float* lossp = nullptr;     // inside scratch: fused-MSE per-workgroup loss partials
   int nlossp = 0;
   float* loss_dst = nullptr;  // set during p3d_train_fwd_bwd: the backward folds the loss here
   const AdamFuse* fuse_adam = nullptr;  // set during p3d_train_step: Adam fused into the backward
@@ -1370,8 +1382,11 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   m->dout[0] = cur; cur += pad64(Bp * L);
   m->dout[1] = cur; cur += pad64(Bp * L);
-  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + 4 * 2 * (int64_t)L + 64 +
-                            pad64((int64_t)c.max_batch * c.output_size);
+  // split BN-train partials [R][L][2] and fused-MSE loss partials for R = max_batch/16 row tiles
+  const int64_t R_max = (c.max_batch + 15) / 16;
+  const int64_t nlossp_max = pad64(R_max * ((c.output_size + 15) / 16));
+  const int64_t scratch_n = (int64_t)P3D_MAX_W * DOT_CHUNKS + 2 * 64 + R_max * 2 * (int64_t)L + nlossp_max +
+                            pad64((int64_t)c.max_batch * ((c.output_size + 15) / 16 * 16));
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if ((e = hipMemset(m->scratch, 0, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev);
@@ -1391,9 +1406,9 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   m->wsq = m->scratch + P3D_MAX_W * DOT_CHUNKS;
   m->gw = m->wsq + 64;
-  m->bnpart = m->gw + 64;   // [4 row tiles][L][2]: split BN-train partial moments / sums
-  m->lossp = m->bnpart + 4 * 2 * (int64_t)L;
-  m->dybuf = m->lossp + 64;
+  m->bnpart = m->gw + 64;   // [R_max row tiles][L][2]: split BN-train partial moments / sums
+  m->lossp = m->bnpart + R_max * 2 * (int64_t)L;
+  m->dybuf = m->lossp + nlossp_max;
   // TF defaults: BN gamma = 1, moving_variance = 1 (beta/mean = 0 already)
   if (c.batch_norm) {
     std::vector<float> ones(L, 1.0f);
@@ -1724,8 +1739,8 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
   if (ws_row + B > c.max_batch)
     return fail(P3D_ERR_ARG, "p3d_forward: batch " + std::to_string(B) + " (+ workspace row " + std::to_string(ws_row) +
                                  ") exceeds max_batch " + std::to_string(c.max_batch));
-  if (training && c.batch_norm && B > 64)
-    return fail(P3D_ERR_ARG, "p3d_forward: training with batch_norm supports B <= 64 in this build");
+  if (training && c.batch_norm && B > 64 && !m->train_split)
+    return fail(P3D_ERR_ARG, "p3d_forward: the whole-batch BN-train kernels (P3D_TRAIN_SPLIT=0) need B <= 64");
   if (!(keep_prob > 0.f && keep_prob <= 1.f)) return fail(P3D_ERR_ARG, "keep_prob must be in (0, 1]");
   if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_forward: x must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
@@ -1855,7 +1870,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (!m || !dy) return fail(P3D_ERR_ARG, "p3d_backward: null argument");
   if (!m->have_cache) return fail(P3D_ERR_STATE, "p3d_backward: no training forward to differentiate");
   if (B != m->B_cached) return fail(P3D_ERR_ARG, "p3d_backward: batch differs from the training forward");
-  if (B > 64) return fail(P3D_ERR_ARG, "p3d_backward: B <= 64 in this build");
+  if (B > 64 && !m->train_split)
+    return fail(P3D_ERR_ARG, "p3d_backward: the whole-batch kernels (P3D_TRAIN_SPLIT=0) need B <= 64");
   const p3d_cfg& c = m->cfg;
   hipStream_t st = (hipStream_t)stream;
   // dy enters the output layer's GEMMs as a row-major operand read in 16-column groups:
@@ -1997,7 +2013,7 @@ extern "C" int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, i
                                  void* stream) {
   if (!m || !x || !t || !y || !loss_dev) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: null argument");
   if (m->cfg.dtype != P3D_DTYPE_F32) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: bf16 models are inference-only");
-  if (B <= 0 || B > 64) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: B must be in 1..64");
+  if (B <= 0 || B > m->cfg.max_batch) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: B must be in 1..max_batch");
   if (!aligned16(t)) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd: t must be 16-byte aligned");
   int rc = forward_impl(m, x, B, y, 1, keep_prob, seed, P3D_CTR_GLOBAL_STEP, row_offset, 0, stream, t);
   if (rc) return rc;

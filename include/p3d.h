@@ -116,7 +116,7 @@ int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stream);
 
 /* p3d_forward(training = 1, ctr = P3D_CTR_GLOBAL_STEP) + p3d_mse + p3d_backward in one
  * call (session.run of the train op up to compute_gradients, linear_model.py:129,143):
- * x [B,32], t [B,48] device row-major, B <= 64; outputs y [B,48]; loss_dev = mean((y-t)^2);
+ * x [B,32], t [B,48] device row-major, 1 <= B <= max_batch; outputs y [B,48]; loss_dev = mean((y-t)^2);
  * gradients in the flat grads buffer.  The MSE runs in the output layer's epilogue. */
 int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
                       float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,

@@ -171,6 +171,31 @@ def test_train_steps_track_oracle(split, monkeypatch):
     m.close()
 
 
+@pytest.mark.parametrize("B", [128, 200])
+def test_train_steps_beyond_batch_64(B):
+    """--batch_size > 64 (the reference takes any batch): BN over more than four row tiles
+    in k_bn_fwd / k_bn_bwd, loss partials of R row tiles; 3 steps + gradients vs the oracle."""
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=True, batch_norm=True)
+    _grad_check(cfg, 0.5, B)
+    st, m = make(cfg, batch=B, lr=1e-3)
+    rng = np.random.default_rng(23)
+    for step in range(3):
+        x = rng.standard_normal((B, 32))
+        t = rng.standard_normal((B, 48))
+        loss, _, _, out = m.step(None, x, t, 0.5, isTraining=True)
+        rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
+        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=1e-3, rtol=1e-3)
+    w = m.get_weights()
+    for name in m.trainable_names():
+        if "/b1" in name or "/b2_" in name or "/b3_" in name:
+            continue
+        assert np.abs(w[name] - st.params[name]).max() < 5e-5, name
+    for k, v in st.moving.items():
+        close(m.variable(k).cpu().numpy(), v, atol=2e-5, rtol=2e-5)
+    m.close()
+
+
 def test_predict14_gradients_and_train_steps():
     """--predict_14 (42 outputs, not a multiple of 16): backward through the zero-padded dy
     path and the fused-MSE train step, vs the oracle."""
