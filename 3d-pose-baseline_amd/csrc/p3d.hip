@@ -1178,6 +1178,7 @@ struct p3d_model {
   int fwd_t = 0;            // inference layers in the transposed-accumulator form (env P3D_FWD_T=1;
                             // bit-identical, +3% single-stream, -2% at 4 streams: 58 vs 52 VGPRs)
   int in_wk = 2, out_wk = 16; // input / output layer variants (env P3D_IN_WK, P3D_OUT_WK; 0 = infer_wk)
+  int out_big = 0;            // output layer tiling at M >= big_m (env P3D_OUT_BIG; 0 = the B <= 64 one)
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
@@ -1393,6 +1394,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
   if (const char* ev = getenv("P3D_FWD_T")) m->fwd_t = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_OUT_BIG")) m->out_big = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
@@ -1564,13 +1566,20 @@ static bool use_big(const p3d_model* m, const FwdArgs& a, int kind, bool whole_b
          a.bn != 2 && !a.z_save && a.ldy == 0;
 }
 
-static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static GemmF32Args big_args(const FwdArgs& a) {
   GemmF32Args g{};
   g.A = a.X; g.Wf = a.Wf; g.bias = a.bias; g.wsq = a.wsq;
   g.M = a.M; g.K = a.K; g.N = a.N;
   g.bn = a.bn; g.gamma = a.gamma; g.beta = a.beta; g.mmean = a.mmean; g.mvar = a.mvar; g.eps = a.eps;
   g.relu = a.relu; g.keep = a.keep; g.seed = a.seed; g.ctr = a.ctr; g.site = a.site; g.row_off = a.row_off;
   g.ctr_dev = a.ctr_dev; g.res = a.res; g.Y = a.Y;
+  return g;
+}
+
+static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
+  const GemmF32Args g = big_args(a);
   const unsigned grid = (unsigned)(((a.M + 127) / 128) * (a.N / 128));
   ProfScope ps(m, "fwd_hidden_big");
   // big_depth selects the LDS ring: 1 -> 1 k-group x 4 stages (64 KB, two workgroups per
@@ -1613,10 +1622,32 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
     LAUNCH_CHECK("k_gemm_f32");
     return P3D_OK;
   }
+  if (kind == 0 && !whole_batch && m->big_m > 0 && a.M >= m->big_m && a.N % 128 == 0 && a.K == 32 &&
+      a.bn != 2 && !a.z_save && a.ldy == 0 && aligned16(a.X)) {
+    // input layer at large M: the 128x128-tile LDS-DMA GEMM, A DMA'd from the row-major input
+    ProfScope ps(m, "fwd_in_big");
+    GemmF32Args g = big_args(a);
+    g.lda = a.ldx;
+    go(ps, k_gemm_f32<2, 2, false>, dim3((unsigned)(((a.M + 127) / 128) * (a.N / 128))), dim3(256), st, g);
+    LAUNCH_CHECK("k_gemm_f32");
+    return P3D_OK;
+  }
   if (kind == 0 && !whole_batch && m->big_m > 0 && a.M >= m->big_m) {
     // input layer (K = 32: two k-groups) at large M: 64 rows x 16 columns per wave
     ProfScope ps(m, "fwd_in_big");
     go(ps, k_fwd<4, 2, 2, 2, false, true, 0>, dim3((a.N + 15) / 16, (a.M + 63) / 64), dim3(128), st, a);
+    LAUNCH_CHECK("k_fwd");
+    return P3D_OK;
+  }
+  if (kind == 2 && !whole_batch && m->big_m > 0 && a.M >= m->big_m && m->out_big && !a.tgt && !a.z_save) {
+    // output layer (N = 48) at large M: several row tiles per wave so each weight fragment
+    // loaded serves 2-4 row tiles (P3D_OUT_BIG selects the tiling)
+    ProfScope ps(m, "fwd_out_big");
+    const int gx = (a.N + 15) / 16;
+    if (m->out_big == 1) go(ps, k_fwd<4, 8, 4, 2, true, false, 2>, dim3(gx, (a.M + 63) / 64), dim3(512), st, a);
+    else if (m->out_big == 2) go(ps, k_fwd<4, 16, 2, 2, true, false, 2>, dim3(gx, (a.M + 63) / 64), dim3(1024), st, a);
+    else if (m->out_big == 3) go(ps, k_fwd<2, 8, 4, 2, true, false, 2>, dim3(gx, (a.M + 31) / 32), dim3(512), st, a);
+    else go(ps, k_fwd<2, 16, 2, 2, true, false, 2>, dim3(gx, (a.M + 31) / 32), dim3(1024), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
   }
@@ -1646,8 +1677,6 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   LAUNCH_CHECK("k_fwd");
   return P3D_OK;
 }
-
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
   const p3d_cfg& c = m->cfg;

@@ -21,7 +21,8 @@
 #include "p3d_bf16.h"   // p3d_wait_stages
 
 struct GemmF32Args {
-  const float* A;            // packed [M, K] activations (ngA = K/16)
+  const float* A;            // packed [M, K] activations (ngA = K/16), or row-major [M, lda] (APK = false)
+  int64_t lda;
   const float* Wf;           // packed [N, K] forward weight
   const float* bias;         // [N]
   const float* wsq;          // max-norm ||W||^2 or null
@@ -35,7 +36,10 @@ struct GemmF32Args {
   float* Y;                  // packed [M, N]
 };
 
-template <int KG, int NST>
+// APK = false: A is the row-major network input (the input layer, K = 32): lane (i, q) of
+// A tile (rt, g) DMAs the 16 B at row 16rt+i (clamped to M-1), columns 16g+4q..+3 -- the same
+// fragment the packed layout holds, so the rest of the kernel is unchanged.
+template <int KG, int NST, bool APK = true>
 __global__ __launch_bounds__(256) void k_gemm_f32(GemmF32Args p) {
   constexpr int STAGE = 16 * KG * 1024;   // 8 A + 8 B tiles per k-group
   constexpr int PER = 4 * KG;             // DMA instructions per wave per stage
@@ -58,6 +62,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmF32Args p) {
   // the PER tiles this wave DMAs per stage: source base (k-group 0) and LDS slot
   const unsigned char* src[PER];
   int slot[PER];
+  int64_t sstep[PER];                     // source bytes per stage (KG k-groups)
 #pragma unroll
   for (int c = 0; c < PER; ++c) {
     const int t = w * PER + c;            // 0 .. 16*KG-1
@@ -66,14 +71,22 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmF32Args p) {
     const int jt = tt / KG, g = tt % KG;  // row tile jt (0..7) of the panel, k-group g
     int rt = isB ? 8 * nt + jt : 8 * mt + jt;
     if (!isB) rt = rt < rt_last ? rt : rt_last;   // tiles past M re-read the last one
-    src[c] = (const unsigned char*)(isB ? p.Wf : p.A) + ((int64_t)rt * ngA + g) * 1024 + lane * 16;
+    if (isB || APK) {
+      src[c] = (const unsigned char*)(isB ? p.Wf : p.A) + ((int64_t)rt * ngA + g) * 1024 + lane * 16;
+      sstep[c] = (int64_t)KG * 1024;
+    } else {
+      int row = 16 * rt + (lane & 15);
+      row = row < p.M ? row : p.M - 1;
+      src[c] = (const unsigned char*)(p.A + (int64_t)row * p.lda + 16 * g + 4 * (lane >> 4));
+      sstep[c] = (int64_t)KG * 64;
+    }
     slot[c] = t * 1024;
   }
   auto issue = [&](int ks, int buf) {
     unsigned char* base = smem + buf * STAGE;
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      __builtin_amdgcn_global_load_lds((const void*)(src[c] + (int64_t)ks * KG * 1024), (void*)(base + slot[c]),
+      __builtin_amdgcn_global_load_lds((const void*)(src[c] + (int64_t)ks * sstep[c]), (void*)(base + slot[c]),
                                        16, 0, 0);
   };
 
