@@ -19,6 +19,7 @@
 #include "p3d_eval.h"
 #include "p3d_gemm.h"
 #include "p3d_data.h"
+#include "p3d_serve.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -162,7 +163,6 @@ struct FwdArgs {
 
 // Phase timestamps for kernel development (build with -DP3D_TRACE; tools/trace_train.py).
 #ifdef P3D_TRACE
-__device__ unsigned long long g_p3d_trace[4096 * 8];
 #define P3D_STAMP(k)                                                                             \
   do {                                                                                           \
     if ((threadIdx.x & 63) == 0 && (blockIdx.x + gridDim.x * blockIdx.y) < 4096)                 \
@@ -1182,6 +1182,16 @@ struct p3d_model {
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
+  // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
+  // census/barrier words and the spin-timeout flag; allocated at the first call
+  float* serve_buf = nullptr;
+  unsigned* serve_sync = nullptr;
+  int* serve_err = nullptr;
+  int serve_grid = 0;
+  int serve_groups = 8;     // XCD groups that take steps (env P3D_SERVE_GROUPS)
+  int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
+  int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
+  int serve_w4 = 0;         // 1: k_serve4 (4-wave workgroups, 512 registers per wave; env P3D_SERVE_W4)
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -1225,6 +1235,8 @@ void free_all(p3d_model* m) {
   if (m->wbf) (void)hipFree(m->wbf);
   if (m->aff) (void)hipFree(m->aff);
   if (m->abf) (void)hipFree(m->abf);
+  if (m->serve_buf) (void)hipFree(m->serve_buf);
+  if (m->serve_sync) (void)hipFree(m->serve_sync);
 }
 }  // namespace
 
@@ -1400,6 +1412,10 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_KS")) m->serve_ks = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_W4")) m->serve_w4 = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   {
     StepState s0{};
     s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
@@ -1844,6 +1860,115 @@ extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, in
   return p3d_forward_ex(m, x, B, y, training, keep_prob, seed, ctr, row_offset, 0, stream);
 }
 
+// ---- persistent XCD-local evaluation (k_serve, p3d_serve.h) ---------------------------
+// k_serve variant (env P3D_SERVE_KS = K slices 8 | 4, P3D_SERVE_DEPTH = register-ring depth):
+// each wave's ngL/KS k-groups must be a multiple of the depth, else the depth drops to 1
+static int serve_depth_for(const p3d_model* m, int L, int ks) {
+  const int ng = L / 16 / ks;
+  int d = m->serve_depth;
+  if (d != 1 && d != 2 && d != 3 && d != 4 && d != 8) d = 2;
+  if (d > 4 && !m->serve_w4) d = 4;
+  if (d == 3 && m->serve_w4) d = 2;
+  while (d > 1 && ng % d != 0) --d;
+  return d;
+}
+
+template <int NDT>
+static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
+  if (m->serve_w4) {   // 4-wave workgroups, one wave per SIMD (k_serve4); K slices of ngL/4 k-groups
+    const int d = serve_depth_for(m, a.L, 4);
+    if (d == 8) go(ps, k_serve4<8, NDT>, dim3(grid), dim3(256), st, a);
+    else if (d == 4) go(ps, k_serve4<4, NDT>, dim3(grid), dim3(256), st, a);
+    else if (d == 2) go(ps, k_serve4<2, NDT>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_serve4<1, NDT>, dim3(grid), dim3(256), st, a);
+    return;
+  }
+  const int ks = m->serve_ks == 4 ? 4 : 8;
+  const int d = serve_depth_for(m, a.L, ks);
+  if (ks == 8) {
+    if (d == 4) go(ps, k_serve<4, NDT, 8>, dim3(grid), dim3(512), st, a);
+    else if (d == 3) go(ps, k_serve<3, NDT, 8>, dim3(grid), dim3(512), st, a);
+    else if (d == 2) go(ps, k_serve<2, NDT, 8>, dim3(grid), dim3(512), st, a);
+    else go(ps, k_serve<1, NDT, 8>, dim3(grid), dim3(512), st, a);
+  } else {
+    if (d == 4) go(ps, k_serve<4, NDT, 4>, dim3(grid), dim3(512), st, a);
+    else if (d == 2) go(ps, k_serve<2, NDT, 4>, dim3(grid), dim3(512), st, a);
+    else go(ps, k_serve<1, NDT, 4>, dim3(grid), dim3(512), st, a);
+  }
+}
+
+extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream) {
+  if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_serve: null argument");
+  const p3d_cfg& c = m->cfg;
+  if (B <= 0) return fail(P3D_ERR_ARG, "p3d_serve: batch must be positive");
+  if (c.dtype != P3D_DTYPE_F32) return fail(P3D_ERR_ARG, "p3d_serve: fp32 models only");
+  if (c.linear_size % 128 != 0 || c.input_size > 64 || c.output_size > 64 ||
+      2 * c.num_layers + 2 > P3D_SERVE_MAXL)
+    return fail(P3D_ERR_ARG, "p3d_serve: needs linear_size % 128 == 0, input/output size <= 64, <= 7 blocks");
+  if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_serve: x must be 16-byte aligned");
+  if ((B + 63) / 64 > 0x7fffffff) return fail(P3D_ERR_ARG, "p3d_serve: too many rows");
+  hipStream_t st = (hipStream_t)stream;
+  const int L = c.linear_size, U = L / 32, NDT = (c.output_size + 15) / 16;
+  const int64_t slab = (int64_t)64 * L, PT = (int64_t)4 * NDT * 256;
+  hipError_t e;
+  if (!m->serve_buf) {
+    int dev = 0, cus = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    m->serve_grid = cus;   // one 512-thread workgroup per CU (the LDS ring admits one)
+    const int64_t nbuf = 8 * 3 * slab + 8 * 2 * (int64_t)U * PT;
+    if ((e = hipMalloc(&m->serve_buf, nbuf * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    if ((e = hipMemset(m->serve_buf, 0, nbuf * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    if ((e = hipMalloc(&m->serve_sync, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    if ((e = hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    m->serve_err = (int*)(m->serve_sync + P3D_SERVE_SYNC_WORDS);
+  }
+  ServeArgs a{};
+  a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);
+  a.L = L; a.K0 = c.input_size; a.ND = c.output_size; a.nblk = c.num_layers;
+  a.bn = c.batch_norm; a.residual = c.residual; a.eps = c.bn_eps;
+  a.act = m->serve_buf; a.part = m->serve_buf + 8 * 3 * slab;
+  a.sync = m->serve_sync; a.err = m->serve_err;
+  a.max_groups = m->serve_groups;
+  for (size_t l = 0; l < m->layers.size(); ++l) {
+    const Layer& ly = m->layers[l];
+    ServeLayer& s = a.ly[l];
+    s.Wf = m->wpk + ly.wf; s.bias = m->flat[0] + ly.b;
+    if (ly.bn) {
+      s.gamma = m->flat[0] + ly.gamma; s.beta = m->flat[0] + ly.beta;
+      s.mmean = m->moving + ly.mmean; s.mvar = m->moving + ly.mvar;
+    }
+    s.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
+  }
+  if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
+    return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+  {
+    ProfScope ps(m, "serve");
+    const unsigned grid = (unsigned)m->serve_grid;
+    if (NDT == 1) launch_serve_k<1>(ps, m, grid, st, a);
+    else if (NDT == 2) launch_serve_k<2>(ps, m, grid, st, a);
+    else if (NDT == 3) launch_serve_k<3>(ps, m, grid, st, a);
+    else launch_serve_k<4>(ps, m, grid, st, a);
+  }
+  LAUNCH_CHECK("k_serve");
+  return P3D_OK;
+}
+
+extern "C" int p3d_serve_check(p3d_model* m) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  if (!m->serve_err) return P3D_OK;
+  int v = 0;
+  hipError_t e = hipMemcpy(&v, m->serve_err, sizeof(int), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
+  if (v) return fail(P3D_ERR_HIP, "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
+  return P3D_OK;
+}
+
 // Timing hook: `reps` back-to-back launches of hidden layer `layer` (1 .. 2N) of the
 // inference forward on workspace rows [0, B) (act[layer-1] -> act[layer]).  Idempotent.
 extern "C" int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream) {
@@ -2187,6 +2312,13 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     }
   } else if (what == 1) {
     n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
+  } else if (what == 3) {
+    const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
+    if (m->serve_w4)
+      n = "k_serve4<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ">";
+    else
+      n = "k_serve<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, ks)) + ", " + std::to_string(ndt) + ", " +
+          std::to_string(ks) + ">";
   } else if (what == 2) {
     n = m->train_split ? "k_fwd<1, 8, 8, 2, true, true, 1>" : "k_fwd<4, 8, 8, 2, true, true, 1>";
   } else {

@@ -21,6 +21,10 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef P3D_TRACE   // development builds only: in-kernel phase timestamps (tools/trace_*.py)
+__device__ unsigned long long g_p3d_trace[4096 * 8];
+#endif
+
 // float offset of element (r, c) in a packed matrix with ng = C/16 column groups
 __device__ __host__ __forceinline__ int64_t p3d_pk(int r, int c, int ng) {
   return (((int64_t)(r >> 4) * ng + (c >> 4)) << 8) + (((r & 15) + ((c & 15) >> 2) * 16) << 2) + (c & 3);

@@ -1,0 +1,769 @@
+// p3d_serve.h -- persistent XCD-local inference of the pose-lifting network at batch 64.
+//
+// The reference evaluates as a sequence of independent batch-64 steps
+// (src/predict_3dpose.py:352-444 calling LinearModel.step, src/linear_model.py:203-245).
+// Run as one kernel chain per step (k_fwd, six launches), a step is bound by per-launch
+// fixed costs (dispatch, operand latency, drain: ~4.5 us per layer for 0.85 us of MFMA
+// work).  k_serve instead keeps the whole network of a step inside ONE XCD:
+//
+//   * grid = one 512-thread workgroup per CU.  Each workgroup reads its XCD id
+//     (s_getreg HW_REG_XCC_ID) and joins that XCD's group (census: one returning atomic);
+//     a one-time fan-in waits until every workgroup is resident and the census is final.
+//   * the groups take the launch's batch-64 steps round-robin (step b -> group b % ngroups);
+//     a group runs its steps one after another, every layer of a step spread over its ~32
+//     CUs: unit u = 64 rows x 32 output columns (column tiles 2u, 2u+1).  The contraction
+//     of a unit is split over the 8 waves (2 column tiles x 4 K-quarters), each wave
+//     running four row tiles with a register ring of operand fragments loaded straight
+//     from L2 (fragment-major 1 KB tiles, p3d_kernels.h: every operand byte is loaded once
+//     per CU, no LDS staging); the K-quarter partials meet in LDS and are summed in fixed
+//     order.  The product is transposed, so the epilogue (max-norm scale, bias, eval BN,
+//     ReLU, residual) works on float4s and stores whole 1 KB tiles.
+//   * layer -> layer hand-off stays inside the XCD's L2: producers store plainly (the L1 is
+//     write-through), drain (s_waitcnt vmcnt(0)) and publish a per-member phase flag (plain
+//     store: it lands in the same L2); consumers poll the members' flags and read the
+//     activations with sc1 loads (L1 bypass, served by the shared L2).  Grouping by the
+//     XCD id read from the hardware -- not by blockIdx -- is what makes that hand-off valid.
+//   * the next layer's weight fragments (which do not depend on the hand-off) are loaded
+//     into the ring between the drain and the flag poll, so their latency hides under the
+//     barrier; bias / BN / residual / W4 operands are loaded before the contraction.
+//   * the output layer (N = 48) is fused into the last hidden layer's epilogue: every unit
+//     multiplies its 64 x 32 slice of the block output by the matching 32 rows of W4 and
+//     stores a 64 x 48 partial; the next phase (the next step's input layer) sums the
+//     partials in fixed unit order (deterministic) and writes y = sum / maxnorm + b4.
+//
+// Phases per step: input layer (+ the previous step's output reduction), then the 2N
+// hidden layers, one group barrier after each.  Results are those of a batch-64 forward
+// (eval BN, keep_prob 1), deterministic and independent of where the workgroups land.
+#pragma once
+#include "p3d_kernels.h"
+
+#define P3D_SERVE_MAXL 16          // input + 2*blocks + output layers
+#define P3D_SERVE_SYNC_WORDS 640   // [0..7] census, [8] arrivals, [64 + 64*x + r] flag of member r of group x
+#define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
+#ifndef P3D_SERVE_PREFETCH_B       // request the next layer's weight fragments inside the barrier
+#define P3D_SERVE_PREFETCH_B 1
+#endif
+#ifndef P3D_SERVE_EPI_EARLY        // bias / BN / residual / W4 operands requested before the contraction
+#define P3D_SERVE_EPI_EARLY 1
+#endif
+
+// Phase timestamps for development (-DP3D_TRACE, tools/trace_serve.py): workgroup rank 0
+// (and rank 1) of every XCD group, first 8 local steps, up to 8 stamps per phase (0 begin,
+// 1 compute done, 2 barrier passed, 3 contraction done, 4 K-partials combined) into
+// g_p3d_trace (p3d_kernels.h).
+#ifdef P3D_TRACE
+#define P3D_SERVE_TR(xcc, r, jl, ph) \
+  (((r) < 2 && (jl) < 8 && (ph) < 16) ? g_p3d_trace + 8192 + (r) * 8192 + ((((xcc) * 8 + (jl)) * 16 + (ph)) * 8) : nullptr)
+#define P3D_SERVE_STAMP(tr, k)                                  \
+  do {                                                          \
+    if ((tr) && threadIdx.x == 0) (tr)[k] = wall_clock64();     \
+  } while (0)
+#else
+#define P3D_SERVE_TR(xcc, r, jl, ph) ((unsigned long long*)nullptr)
+#define P3D_SERVE_STAMP(tr, k) do { (void)(tr); } while (0)
+#endif
+
+struct ServeLayer {
+  const float* Wf;     // packed forward weight [N, K] (ngK = K/16 groups per column tile)
+  const float* bias;
+  const float* gamma; const float* beta; const float* mmean; const float* mvar;
+  const float* wsq;    // max-norm ||W||^2 or null
+};
+
+struct ServeArgs {
+  const float* x;      // [M, K0] row-major network input
+  float* y;            // [M, ND] row-major output
+  int64_t M;           // rows; step b covers rows [64b, 64b + 64)
+  int nb;              // steps = ceil(M / 64)
+  int L, K0, ND, nblk; // linear_size, input_size (<= 64), output_size (<= 64), residual blocks
+  int bn, residual; float eps;
+  float* act;          // [8][3][64 * L] packed activations per XCD group
+  float* part;         // [8][2][U][4 * NDT * 256] output partials per XCD group (step parity)
+  unsigned* sync;      // P3D_SERVE_SYNC_WORDS, zeroed before every launch
+  int* err;            // set to 1 when a bounded spin ran out
+  int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
+  ServeLayer ly[P3D_SERVE_MAXL];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+// 16-B load with sc1 (bypasses this CU's L1; served by the XCD's L2): every read of data
+// another CU of the group produced goes through this
+__device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
+}
+
+// ---- register ring -------------------------------------------------------------------
+// The unit's contraction (64 rows x 32 columns x L) is split over the 8 waves along K.
+//   KS = 8: wave w owns k-groups [w*ngL/8, (w+1)*ngL/8) of all 4 row tiles x 2 column
+//           tiles: per k-group 4 A + 2 B fragments for 32 MFMAs, every operand byte loaded
+//           once per CU (384 KB per layer at L = 1024).
+//   KS = 4: wave (kq, ct) owns k-groups [kq*ngL/4, ..) of the 4 row tiles of column tile
+//           ct: 4 A + 1 B per 16 MFMAs, A loaded by both waves of a K-quarter.
+template <int DEPTH, int KS>
+struct ServeRingA {
+  f32x4 a[DEPTH][4];            // activation fragments of the four row tiles
+};
+template <int DEPTH, int KS>
+struct ServeRingB {
+  f32x4 b[DEPTH][KS / 4];       // weight fragments of this wave's column tile(s)
+};
+
+template <int KS>
+__device__ __forceinline__ int p3d_ring_gb(int ngL) {
+  const int w = threadIdx.x >> 6;
+  return KS == 8 ? (ngL * w) >> 3 : (ngL * (w >> 1)) >> 2;
+}
+
+// wave's first weight fragment: column tile 2u (KS = 8) or 2u + ct (KS = 4)
+template <int KS>
+__device__ __forceinline__ const f32x4* p3d_ring_bptr(const float* Wf, int u, int ngL) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ct0 = KS == 8 ? 0 : (w & 1);
+  return (const f32x4*)Wf + ((int64_t)(2 * u + ct0) * ngL + p3d_ring_gb<KS>(ngL)) * 64 + lane;
+}
+
+template <int DEPTH, int KS>
+__device__ __forceinline__ void p3d_ring_load_b(ServeRingB<DEPTH, KS>& R, const float* Wf, int u, int ngL) {
+  const f32x4* pb = p3d_ring_bptr<KS>(Wf, u, ngL);
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int c = 0; c < KS / 4; ++c) R.b[d][c] = pb[(c * ngL + d) * 64];
+}
+
+template <int DEPTH, int KS>
+__device__ __forceinline__ void p3d_ring_load_a(ServeRingA<DEPTH, KS>& R, const float* A, int ngL) {
+  const int lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
+  const int aoff0 = (p3d_ring_gb<KS>(ngL) * 64 + lane) * 16, rstride = ngL * 1024;
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) R.a[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+}
+
+// The unit's contraction, the ring's first DEPTH k-groups already requested.  The wave's
+// ngL/KS k-groups are a multiple of DEPTH (host): straight-line rounds, so the compiler
+// tracks the ring's loads exactly (vmcnt(N) waits, no drain at a loop head).  Returns this
+// wave's tile (row tile w >> 1, column tile 2u + (w & 1)) in the transposed layout, its
+// KS K-slice partials summed in slice order (deterministic).
+template <int DEPTH, int KS>
+__device__ __forceinline__ f32x4 p3d_ring_run(ServeRingA<DEPTH, KS>& RA, ServeRingB<DEPTH, KS>& RB, const float* A,
+                                              const float* Wf, int u, int ngL, f32x4* red, unsigned long long* tr) {
+  constexpr int NC = KS / 4;     // column tiles per wave
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kq = KS == 8 ? w : (w >> 1), ct0 = KS == 8 ? 0 : (w & 1);
+  const int ng = ngL / KS;
+  const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
+  const int aoff0 = (p3d_ring_gb<KS>(ngL) * 64 + lane) * 16, rstride = ngL * 1024;
+  const f32x4* pb = p3d_ring_bptr<KS>(Wf, u, ngL);
+  f32x4 acc[NC][4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifndef P3D_SERVE_DIAG_A   // diagnostic builds (tools/trace_serve.py): re-read early k-groups
+#define P3D_SERVE_DIAG_A(g) (g)
+#endif
+#ifndef P3D_SERVE_DIAG_B
+#define P3D_SERVE_DIAG_B(g) (g)
+#endif
+  for (int g0 = 0; g0 < ng - DEPTH; g0 += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(RB.b[d][c][e], RA.a[d][t][e], acc[c][t], 0, 0, 0);
+      const int gn = g0 + DEPTH + d;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) RA.a[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + P3D_SERVE_DIAG_A(gn) * 1024);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) RB.b[d][c] = pb[(c * ngL + P3D_SERVE_DIAG_B(gn)) * 64];
+      // keep the refill of slot d here, ahead of slot d+1's MFMAs: left alone the scheduler
+      // sinks every refill to the end of the round, exposing the full load latency there
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(RB.b[d][c][e], RA.a[d][t][e], acc[c][t], 0, 0, 0);
+  P3D_SERVE_STAMP(tr, 3);
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) red[((kq * 4 + t) * 2 + ct0 + c) * 64 + lane] = acc[c][t];
+  __syncthreads();
+  P3D_SERVE_STAMP(tr, 4);
+  f32x4 s = red[w * 64 + lane];   // slice 0, tile (w >> 1, w & 1)
+#pragma unroll
+  for (int k = 1; k < KS; ++k) s += red[(k * 8 + w) * 64 + lane];
+  __syncthreads();
+  return s;
+}
+
+// ---- epilogue: lane (j, q) of the tile holds row 16rt + j, columns n0 .. n0+3 ---------
+struct ServeEpi {
+  f32x4 b, inv, shift;
+  float mx;
+};
+
+// Loaded (and the BN factors formed) before the contraction, so neither the loads nor
+// the divides sit between the contraction and the stores.  Same arithmetic as
+// k_gemm_f32's / k_fwd's epilogue: inv = gamma / sqrt(var + eps), shift = beta - mean*inv.
+__device__ __forceinline__ ServeEpi p3d_epi_load(const ServeLayer& ly, int n0, int bn, float eps) {
+  ServeEpi e;
+  e.mx = ly.wsq ? fmaxf(sqrtf(*ly.wsq), 1.0f) : 1.0f;
+  e.b = *(const f32x4*)(ly.bias + n0);
+  e.inv = f32x4{1.f, 1.f, 1.f, 1.f};
+  e.shift = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (bn) {
+    const f32x4 g = *(const f32x4*)(ly.gamma + n0), be = *(const f32x4*)(ly.beta + n0);
+    const f32x4 mu = *(const f32x4*)(ly.mmean + n0), va = *(const f32x4*)(ly.mvar + n0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      e.inv[k] = (1.0f / sqrtf(va[k] + eps)) * g[k];
+      e.shift[k] = be[k] - mu[k] * e.inv[k];
+    }
+  }
+  return e;
+}
+
+// z = acc / maxnorm + b; y = relu(z * inv + shift)
+__device__ __forceinline__ f32x4 p3d_epi_apply(const ServeEpi& ep, f32x4 acc, bool wsq, int bn) {
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float z = (wsq ? acc[e] / ep.mx : acc[e]) + ep.b[e];
+    o[e] = fmaxf(bn ? z * ep.inv[e] + ep.shift[e] : z, 0.0f);
+  }
+  return o;
+}
+
+// W4 fragments (k-group ctg, output tiles o) for the fused output layer
+template <int NDT>
+__device__ __forceinline__ void p3d_wo_load(const ServeLayer& lo, int ctg, int ngL, f32x4 (&wo)[NDT]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 0; o < NDT; ++o) wo[o] = *(const f32x4*)(lo.Wf + ((int64_t)(o * ngL + ctg) * 64 + lane) * 4);
+}
+
+// Output-layer partial of one unit: y (this wave's tile, A-fragment of k-group ctg) times
+// W4 rows 16ctg.. -> NDT 16x16 tiles; the two waves of a row tile combine through LDS
+// (wave ct = 1 hands over, ct = 0 adds in fixed order and stores).  All waves call it.
+template <int NDT>
+__device__ __forceinline__ void p3d_serve_partial(const f32x4 (&wo)[NDT], f32x4 yv, int rt, int ct, f32x4* xch,
+                                                  float* pdst) {
+  const int lane = threadIdx.x & 63;
+  f32x4 acc[NDT];
+#pragma unroll
+  for (int o = 0; o < NDT; ++o) {
+    acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[o] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[o][e], acc[o], 0, 0, 0);
+  }
+  if (ct == 1) {
+#pragma unroll
+    for (int o = 0; o < NDT; ++o) xch[(rt * NDT + o) * 64 + lane] = acc[o];
+  }
+  __syncthreads();
+  if (ct == 0) {
+#pragma unroll
+    for (int o = 0; o < NDT; ++o) {
+      const f32x4 v = acc[o] + xch[(rt * NDT + o) * 64 + lane];
+      *(f32x4*)(pdst + ((rt * NDT + o) * 64 + lane) * 4) = v;
+    }
+  }
+  __syncthreads();
+}
+
+// Output of one step from its partials: y[row, col] = (sum_u part[u]) / maxnorm + b4.
+// Partial element e4 = (tile (rt, o), lane (i, q)) holds rows 16rt + 4q + r, column 16o + i.
+// This workgroup handles its share [r/n, (r+1)/n) of the float4 elements.
+template <int NDT>
+__device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const ServeLayer& lo, const float* pb, int U,
+                                                 int64_t row0, int r, int n) {
+  constexpr int E4 = 4 * NDT * 64;
+  const int s = (int)(((int64_t)E4 * r) / n), e = (int)(((int64_t)E4 * (r + 1)) / n);
+  const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
+  for (int e4 = s + (int)threadIdx.x; e4 < e; e4 += (int)blockDim.x) {
+  f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+  int u = 0;
+  for (; u + 8 <= U; u += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p3d_ld_sc1(rs, ((u + k) * E4 + e4) * 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += v[k];
+  }
+  for (; u < U; ++u) sum += p3d_ld_sc1(rs, (u * E4 + e4) * 16);
+  const int tile = e4 >> 6, ln = e4 & 63, rt = tile / NDT, o = tile % NDT;
+  const int col = 16 * o + (ln & 15), q = ln >> 4;
+  if (col >= p.ND) continue;
+  const float mx = lo.wsq ? fmaxf(sqrtf(*lo.wsq), 1.0f) : 1.0f;
+  const float bb = lo.bias[col];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = row0 + 16 * rt + 4 * q + k;
+    if (row < p.M) p.y[row * p.ND + col] = (lo.wsq ? sum[k] / mx : sum[k]) + bb;
+  }
+  }
+}
+
+// Phase 0 of a step: the input layer (K0 = input_size, A straight from the row-major
+// input; or, with no blocks, the output partials) and the previous step's output
+// reduction, the first unit's operands requested before the reduction.  Inlined by
+// default; as a call (-DP3D_SERVE_PHASE0_CALL=1) its registers do not crowd the hidden
+// layers' register ring (inlined, deeper rings than 2 spill inside the ring).
+#ifndef P3D_SERVE_PHASE0_CALL
+#define P3D_SERVE_PHASE0_CALL 0
+#endif
+#if P3D_SERVE_PHASE0_CALL
+#define P3D_SERVE_P0_ATTR __noinline__
+#else
+#define P3D_SERVE_P0_ATTR __forceinline__
+#endif
+template <int NDT>
+__device__ P3D_SERVE_P0_ATTR void p3d_serve_phase0(const ServeArgs& p, int r, int n, int64_t row0, bool lastp,
+                                              int64_t prev_row0, const float* prev_part, float* pdst, float* act,
+                                              f32x4* xch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rt = w >> 1, ct = w & 1;
+  const int ngL = p.L >> 4, U = p.L >> 5, ngK0 = p.K0 >> 4;
+  constexpr int PT = 4 * NDT * 256;
+  const ServeLayer& li = p.ly[0];
+  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
+  const bool wsq_any = li.wsq != nullptr;
+  for (int u = r; u < U || u == r; u += n) {
+    const bool has = u < U;
+    const int ctg = 2 * u + ct, n0 = 16 * ctg + 4 * (lane >> 4);
+    f32x4 xa[4], wb[4], wo[NDT];
+    ServeEpi ep;
+    if (has) {
+      int64_t rowc = row0 + 16 * rt + (lane & 15);
+      rowc = rowc < p.M ? rowc : p.M - 1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (g < ngK0) {
+          xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + 4 * (lane >> 4));
+          wb[g] = *(const f32x4*)(li.Wf + ((int64_t)(ctg * ngK0 + g) * 64 + lane) * 4);
+        }
+      ep = p3d_epi_load(li, n0, p.bn, p.eps);
+      if (lastp) p3d_wo_load<NDT>(lo, ctg, ngL, wo);
+    }
+    if (u == r && prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, prev_part, U, prev_row0, r, n);
+    if (!has) break;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g < ngK0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[g][e], xa[g][e], acc, 0, 0, 0);
+    const f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn);
+    if (lastp) p3d_serve_partial<NDT>(wo, yv, rt, ct, xch, pdst + (int64_t)u * PT);
+    else *(f32x4*)(act + ((int64_t)(rt * ngL + ctg) * 64 + lane) * 4) = yv;
+  }
+}
+
+template <int DEPTH, int NDT, int KS>
+__global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[KS * 8 * 64];    // K-slice partials (32 / 64 KB)
+  __shared__ __attribute__((aligned(16))) f32x4 xch[4 * NDT * 64];   // output-partial exchange
+  __shared__ int sh[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rt = w >> 1, ct = w & 1;         // this wave's output tile of a unit
+  const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
+
+  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
+  if (tid == 0) {
+    unsigned xr;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+    const int xcc = (int)(xr & 7u);
+    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int bad = 0, spin = 0;
+    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
+    }
+    sh[0] = xcc; sh[1] = (int)rank;
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[2] = bad;
+  }
+  __syncthreads();
+  if (sh[2]) return;
+  const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
+  int ng = 0, gi = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+    if (sh[8 + x] > 0) { if (x == xcc) gi = ng; ++ng; }
+  if (p.max_groups > 0 && ng > p.max_groups) {
+    ng = p.max_groups;
+    if (gi >= ng) gi = p.nb;   // this group takes no steps
+  }
+  unsigned* flags = p.sync + 64 + 64 * xcc;
+  const int64_t slab = (int64_t)64 * L;
+  float* act = p.act + (int64_t)xcc * 3 * slab;
+  constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
+  float* part = p.part + (int64_t)xcc * 2 * U * PT;
+  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
+  const bool wsq_any = p.ly[0].wsq != nullptr;   // max-norm is all layers or none
+  const int P = 2 * p.nblk + 1;              // phases per step
+  unsigned nsync = 0;
+  bool broken = false;
+  ServeRingB<DEPTH, KS> RB;
+  bool b_ready = false;                      // R.b holds layer ph's first fragments of unit r
+
+  // Group barrier through per-member flags kept in the XCD's L2: drain this workgroup's
+  // stores, then (all waves) request the next layer's weight fragments -- independent of
+  // the hand-off -- then one lane publishes the phase and wave 0 polls every member's flag
+  // (sc1 loads, one lane per member) until all reached it.
+  auto group_sync = [&](int next_ph) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++nsync;
+    if (P3D_SERVE_PREFETCH_B && next_ph > 0 && next_ph < P && r < U) {
+      p3d_ring_load_b(RB, p.ly[next_ph].Wf, r, ngL);
+      b_ready = true;
+    }
+    if (tid < 64) {
+      if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!broken) {
+        int spin = 0;
+        while (true) {
+          const unsigned v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : nsync;
+          if (__all(v >= nsync)) break;
+          if (++spin > P3D_SERVE_SPIN) {
+            broken = true;
+            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  int jl = 0;                                // local step index (partial-buffer parity)
+  int64_t prev_row0 = -1;
+  for (int b = gi; b < p.nb; b += ng, ++jl) {
+    const int64_t row0 = (int64_t)b * 64;
+    int cur = 0;                             // buffer holding the current block input
+    for (int ph = 0; ph < P; ++ph) {
+      unsigned long long* tr = P3D_SERVE_TR(xcc, r, jl, ph);
+      P3D_SERVE_STAMP(tr, 0);
+      const bool lastp = (ph == P - 1);
+      float* pdst = part + (int64_t)(jl & 1) * U * PT;
+      if (ph == 0) {
+        p3d_serve_phase0<NDT>(p, r, n, row0, lastp, prev_row0, part + (int64_t)((jl - 1) & 1) * U * PT, pdst, act,
+                              xch);
+      } else {
+        // ---- hidden layer ph (block (ph-1)/2, first or second linear) ----------------
+        const ServeLayer& ly = p.ly[ph];
+        const bool second = ((ph - 1) & 1) == 1;
+        const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
+        const float* A = act + (second ? t1 : cur) * slab;
+        float* Y = act + (second ? t2 : t1) * slab;
+        const float* res = (second && p.residual) ? act + cur * slab : nullptr;
+        for (int u = r; u < U; u += n) {
+          const int ctg = 2 * u + ct, n0 = 16 * ctg + 4 * (lane >> 4);
+          const int64_t off = ((int64_t)(rt * ngL + ctg) * 64 + lane) * 4;
+          if (!(b_ready && u == r)) p3d_ring_load_b(RB, ly.Wf, u, ngL);
+          ServeRingA<DEPTH, KS> RA;
+          p3d_ring_load_a(RA, A, ngL);
+          ServeEpi ep;
+          f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f}, wo[NDT];
+          if (P3D_SERVE_EPI_EARLY) {
+            ep = p3d_epi_load(ly, n0, p.bn, p.eps);
+            if (res) rv = p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4));
+            if (lastp) p3d_wo_load<NDT>(lo, ctg, ngL, wo);
+          }
+          const f32x4 acc = p3d_ring_run(RA, RB, A, ly.Wf, u, ngL, red, tr);
+          if (!P3D_SERVE_EPI_EARLY) {
+            ep = p3d_epi_load(ly, n0, p.bn, p.eps);
+            if (res) rv = p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4));
+            if (lastp) p3d_wo_load<NDT>(lo, ctg, ngL, wo);
+          }
+          f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn);
+          if (res) yv += rv;
+          if (lastp) p3d_serve_partial<NDT>(wo, yv, rt, ct, xch, pdst + (int64_t)u * PT);
+          else *(f32x4*)(Y + off) = yv;
+        }
+        b_ready = false;
+        if (second) cur = t2;
+      }
+      P3D_SERVE_STAMP(tr, 1);
+      group_sync(ph + 1);
+      P3D_SERVE_STAMP(tr, 2);
+    }
+    prev_row0 = row0;
+  }
+  if (prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
+}
+
+// =====================================================================================
+// k_serve4: the same persistent XCD-local schedule with 4-wave (256-thread) workgroups,
+// one wave per SIMD, so every wave has the full 512-entry register file (arch VGPRs +
+// AGPRs).  Wave w owns K slice w of the unit (k-groups [w*ngL/4, (w+1)*ngL/4)) for all
+// 4 row tiles x 2 column tiles: per k-group 4 A + 2 B fragments (each operand byte loaded
+// once per CU: 384 KB per layer at L = 1024) for 32 MFMAs on 8 independent accumulators,
+// with a DEPTH-deep register ring.  After the K-slice combine (LDS, slice order) wave w
+// owns row tile w of both column tiles, so the fused output-layer partial of a row tile
+// needs no exchange.
+// =====================================================================================
+template <int DEPTH, int NDT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve4(ServeArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 8 * 64];     // [slice][rt*2 + ct][lane] (32 KB)
+  __shared__ int sh[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
+  const int q4 = 4 * (lane >> 4);
+
+  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
+  if (tid == 0) {
+    unsigned xr;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+    const int xcc = (int)(xr & 7u);
+    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int bad = 0, spin = 0;
+    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
+    }
+    sh[0] = xcc; sh[1] = (int)rank;
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[2] = bad;
+  }
+  __syncthreads();
+  if (sh[2]) return;
+  const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
+  int ng = 0, gi = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+    if (sh[8 + x] > 0) { if (x == xcc) gi = ng; ++ng; }
+  if (p.max_groups > 0 && ng > p.max_groups) {
+    ng = p.max_groups;
+    if (gi >= ng) gi = p.nb;   // this group takes no steps
+  }
+  unsigned* flags = p.sync + 64 + 64 * xcc;
+  const int64_t slab = (int64_t)64 * L;
+  float* act = p.act + (int64_t)xcc * 3 * slab;
+  constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
+  float* part = p.part + (int64_t)xcc * 2 * U * PT;
+  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
+  const bool wsq_any = p.ly[0].wsq != nullptr;   // max-norm is all layers or none
+  const int P = 2 * p.nblk + 1;              // phases per step
+  unsigned nsync = 0;
+  bool broken = false;
+  const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
+
+  auto group_sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++nsync;
+    if (tid < 64) {
+      if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!broken) {
+        int spin = 0;
+        while (true) {
+          const unsigned v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : nsync;
+          if (__all(v >= nsync)) break;
+          if (++spin > P3D_SERVE_SPIN) {
+            broken = true;
+            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  // output-layer partial of row tile w: y[c] (A-fragments of k-groups 2u + c) x W4
+  auto partial = [&](const f32x4 (&yv)[2], const f32x4 (&wo)[2][NDT], float* pd) {
+#pragma unroll
+    for (int o = 0; o < NDT; ++o) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[c][e], wo[c][o][e], acc, 0, 0, 0);
+      *(f32x4*)(pd + ((w * NDT + o) * 64 + lane) * 4) = acc;
+    }
+  };
+
+  int jl = 0;
+  int64_t prev_row0 = -1;
+  for (int b = gi; b < p.nb; b += ng, ++jl) {
+    const int64_t row0 = (int64_t)b * 64;
+    int cur = 0;
+    for (int ph = 0; ph < P; ++ph) {
+      unsigned long long* tr = P3D_SERVE_TR(xcc, r, jl, ph);
+      P3D_SERVE_STAMP(tr, 0);
+      const bool lastp = (ph == P - 1);
+      float* pdst = part + (int64_t)(jl & 1) * U * PT;
+      if (ph == 0) {
+        const ServeLayer& li = p.ly[0];
+        for (int u = r; u < U || u == r; u += n) {
+          const bool has = u < U;
+          f32x4 xa[4], wb[2][4], wo[2][NDT];
+          ServeEpi ep[2];
+          if (has) {
+            int64_t rowc = row0 + 16 * w + (lane & 15);
+            rowc = rowc < p.M ? rowc : p.M - 1;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              if (g < ngK0) {
+                xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                  wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
+              }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              ep[c] = p3d_epi_load(li, 16 * (2 * u + c) + q4, p.bn, p.eps);
+              if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
+            }
+          }
+          if (u == r && prev_row0 >= 0)
+            p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
+          if (!has) break;
+          f32x4 yv[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              if (g < ngK0)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[c][g][e], xa[g][e], acc, 0, 0, 0);
+            yv[c] = p3d_epi_apply(ep[c], acc, wsq_any, p.bn);
+          }
+          if (lastp) partial(yv, wo, pdst + (int64_t)u * PT);
+          else {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) *(f32x4*)(act + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
+          }
+        }
+      } else {
+        const ServeLayer& ly = p.ly[ph];
+        const bool second = ((ph - 1) & 1) == 1;
+        const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
+        const float* A = act + (second ? t1 : cur) * slab;
+        float* Y = act + (second ? t2 : t1) * slab;
+        const float* res = (second && p.residual) ? act + cur * slab : nullptr;
+        const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
+        const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
+        for (int u = r; u < U; u += n) {
+          const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
+          f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
+#pragma unroll
+          for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + d) * 64];
+          }
+          ServeEpi ep[2];
+          f32x4 rv[2], wo[2][NDT];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int64_t off = ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4;
+            ep[c] = p3d_epi_load(ly, 16 * (2 * u + c) + q4, p.bn, p.eps);
+            rv[c] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+            if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
+          }
+          f32x4 acc[2][4];
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef P3D_TRACE
+          if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memtime();
+#endif
+          for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                  for (int t = 0; t < 4; ++t)
+                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+              const int gn = g0 + DEPTH + d;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + P3D_SERVE_DIAG_A(gn) * 1024);
+#pragma unroll
+              for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + P3D_SERVE_DIAG_B(gn)) * 64];
+              __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
+            }
+          }
+#pragma unroll
+          for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                  acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+          P3D_SERVE_STAMP(tr, 3);
+#ifdef P3D_TRACE
+          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) red[(w * 8 + t * 2 + c) * 64 + lane] = acc[c][t];
+          __syncthreads();
+          P3D_SERVE_STAMP(tr, 4);
+          f32x4 yv[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            f32x4 sacc = red[(w * 2 + c) * 64 + lane];   // slice 0, tile (w, c)
+#pragma unroll
+            for (int k = 1; k < 4; ++k) sacc += red[(k * 8 + w * 2 + c) * 64 + lane];
+            yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn);
+            if (res) yv[c] += rv[c];
+          }
+          __syncthreads();
+          if (lastp) partial(yv, wo, pdst + (int64_t)u * PT);
+          else {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
+          }
+        }
+        if (second) cur = t2;
+      }
+      P3D_SERVE_STAMP(tr, 1);
+      group_sync();
+      P3D_SERVE_STAMP(tr, 2);
+    }
+    prev_row0 = row0;
+  }
+  if (prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
+}

@@ -416,6 +416,22 @@ class LinearModel(object):
                                    int(ws_row), self.stream()), "p3d_forward")
         return out
 
+    def serve_device(self, x, out=None):
+        """Evaluation forward of x [B, input_size] as ceil(B/64) independent batch-64 steps
+        (predict_3dpose.py:evaluate_batches' per-batch ``step`` loop, :396) in one persistent
+        launch: each XCD runs whole steps out of its own L2 (p3d_serve, csrc/p3d_serve.h).
+        Eval BN, keep_prob 1; no host sync."""
+        x = self._as_dev(x, self.input_size, "enc_in")
+        B = x.shape[0]
+        if out is None:
+            out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
+        check(lib().p3d_serve(self._h, ptr(x), B, ptr(out), self.stream()), "p3d_serve")
+        return out
+
+    def serve_check(self):
+        """Raise if a p3d_serve launch could not synchronise its workgroups (device read)."""
+        check(lib().p3d_serve_check(self._h), "p3d_serve")
+
     def loss_device(self, y, t, dy=None):
         B = y.shape[0]
         check(lib().p3d_mse(ptr(y), ptr(t), B, self.output_size, ptr(self._loss_dev),

@@ -104,6 +104,19 @@ int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t tr
                    float keep_prob, uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row,
                    void* stream);
 
+/* Evaluation forward of B rows as ceil(B/64) independent batch-64 steps -- the
+ * per-batch LinearModel.step(isTraining=False) loop of predict_3dpose.py:evaluate_batches
+ * (:352-444, step at :396) -- in ONE persistent launch (k_serve): each XCD runs whole
+ * steps (all layers) out of its own L2, steps dealt round-robin over the XCDs.  Eval BN,
+ * keep_prob 1; x [B, input_size], y [B, output_size] device pointers.  fp32 models with
+ * linear_size % 128 == 0, input_size <= 64, output_size <= 64, at most 7 blocks.
+ * Results equal p3d_forward's to fp32 rounding (the output layer sums 32-column partials
+ * in fixed order; deterministic).  Returns P3D_ERR_HIP if the device never ran every
+ * workgroup of the launch together (reported by the next p3d_serve_check). */
+int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
+/* 0 if every p3d_serve launch so far completed its synchronisation (device read; syncs). */
+int p3d_serve_check(p3d_model* m);
+
 /* MSE loss of linear_model.py:129 and its gradient: loss = mean((y-t)^2) over
  * B*D, dy = (1/(B*D)) * 2*(y-t).  loss_dev: one device float (may be NULL),
  * dy may be NULL. */

@@ -1,0 +1,119 @@
+"""p3d_serve (k_serve: persistent XCD-local evaluation of batch-64 steps) vs the oracle.
+
+Reference behaviour: predict_3dpose.py:evaluate_batches (:352-444) runs LinearModel.step
+(linear_model.py:203-245, isTraining=False, keep_prob 1) once per batch of 64; the rows
+of a batch are independent in eval mode, so every output row must equal the oracle's
+eval forward of that row.  Tolerance as tests/test_gpu_parity.py: |d| <= 2e-5 + 2e-5|ref|
+(fp32 MFMA chain vs the fp64 oracle); vs the batch-64 HIP kernels 5e-5 (the output layer
+sums 32-column partials in a different, fixed order).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import linear_model  # noqa: E402
+from oracle import ref_mlp  # noqa: E402
+
+
+def make(cfg, max_batch=64, seed=1, bn_seed=2):
+    st = ref_mlp.init_state(cfg, seed=seed, bn_seed=bn_seed)
+    m = linear_model.LinearModel(cfg.linear_size, cfg.num_layers, cfg.residual, cfg.batch_norm, cfg.max_norm,
+                                 64, 1e-3, "/tmp/p3d_test", cfg.predict_14, seed=11, max_batch=max_batch)
+    m.set_weights({**st.params, **st.moving})
+    return st, m
+
+
+def close(a, b, atol=2e-5, rtol=2e-5):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    err = np.abs(a - b)
+    tol = atol + rtol * np.abs(b)
+    assert np.all(err <= tol), "max err %.3g (at ref %.3g)" % (err.max(), b.flat[np.argmax(err - tol)])
+
+
+def test_serve_cfg2_ragged_vs_oracle():
+    """cfg2 network, 37 full steps + a 13-row tail: oracle, batch-64 kernels, determinism."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    B = 64 * 37 + 13
+    x = np.random.default_rng(3).standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    y = m.serve_device(xd)
+    y2 = m.serve_device(xd)
+    torch.cuda.synchronize()
+    m.serve_check()
+    assert torch.equal(y, y2), "k_serve is not deterministic"
+    ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+    close(y.cpu().numpy(), ro)
+    y64 = torch.cat([m.forward_device(xd[i:i + 64]) for i in range(0, B, 64)])
+    close(y.cpu().numpy(), y64.cpu().numpy(), atol=5e-5, rtol=5e-5)
+    m.close()
+
+
+@pytest.mark.parametrize("L,N,residual,batch_norm,max_norm,p14", [
+    (256, 1, True, True, False, False),      # cfg1
+    (256, 0, False, True, False, False),     # no blocks: the input layer feeds the output partials
+    (256, 3, True, True, True, False),       # max-norm on every weight
+    (512, 2, False, False, False, False),    # no BN, no residual
+    (1024, 2, True, True, False, True),      # --predict_14: 42 outputs
+    (2048, 1, True, True, False, False),     # 64 units per layer: two per workgroup
+])
+def test_serve_variants_vs_oracle(L, N, residual, batch_norm, max_norm, p14):
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
+                      predict_14=p14)
+    st, m = make(cfg)
+    B = 64 * 19 + 5
+    x = np.random.default_rng(L + N).standard_normal((B, 32)).astype(np.float32)
+    y = m.serve_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    m.serve_check()
+    ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+    assert y.shape == ro.shape
+    close(y, ro, atol=5e-5, rtol=5e-5)
+    m.close()
+
+
+def test_serve_small_batches():
+    """Fewer steps than XCD groups (most groups idle), single rows."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    for B in (1, 7, 64, 65, 300):
+        x = np.random.default_rng(B).standard_normal((B, 32)).astype(np.float32)
+        y = m.serve_device(torch.from_numpy(x).cuda()).cpu().numpy()
+        ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+        close(y, ro)
+    m.serve_check()
+    m.close()
+
+
+def test_serve_many_steps_every_row():
+    """2,000 steps (~250 per XCD group, ten thousand group barriers) with distinct rows:
+    every output row vs the large-M HIP path.  A stale hand-off (a layer reading an L1
+    line or a partial from an earlier step) would show up as a wrong row."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg, max_batch=8192)
+    B = 64 * 2000
+    xd = torch.randn((B, 32), device="cuda", generator=torch.Generator("cuda").manual_seed(5))
+    y = m.serve_device(xd)
+    ref = torch.cat([m.forward_device(xd[i:i + 8192]) for i in range(0, B, 8192)])
+    torch.cuda.synchronize()
+    m.serve_check()
+    d = (y - ref).abs()
+    tol = 5e-5 + 5e-5 * ref.abs()
+    assert bool((d <= tol).all()), "max err %.3g" % float(d.max())
+    # and a sample of rows vs the fp64 oracle
+    idx = np.random.default_rng(0).choice(B, 512, replace=False)
+    ro, _ = ref_mlp.forward(st, xd[idx].cpu().numpy(), False, 1.0, 0, 0, 0)
+    close(y[idx].cpu().numpy(), ro)
+    m.close()
+
+
+def test_serve_rejects_bad_shapes():
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    with pytest.raises(ValueError):
+        m.serve_device(torch.zeros((64, 31), device="cuda"))
+    m.close()
