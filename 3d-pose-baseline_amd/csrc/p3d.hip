@@ -1191,7 +1191,7 @@ struct p3d_model {
   int serve_groups = 8;     // XCD groups that take steps (env P3D_SERVE_GROUPS)
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
-  int serve_w4 = 0;         // 1: k_serve4 (4-wave workgroups, 512 registers per wave; env P3D_SERVE_W4)
+  int serve_w4 = 1;         // 1: k_serve4 (4-wave workgroups, 512 registers per wave; env P3D_SERVE_W4)
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;

@@ -579,10 +579,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   bool broken = false;
   const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
 
-  auto group_sync = [&]() {
+  // the next layer's first weight fragments (independent of the hand-off) are requested
+  // between the drain and the flag poll, so their latency hides under the barrier
+  f32x4 rbp[DEPTH][2];
+  bool b_ready = false;
+  auto group_sync = [&](int next_ph) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     ++nsync;
+    if (P3D_SERVE_PREFETCH_B && next_ph > 0 && next_ph < P && r < U) {
+      const f32x4* pbn = (const f32x4*)p.ly[next_ph].Wf + ((int64_t)(2 * r) * ngL + gb) * 64 + lane;
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) rbp[d][c] = pbn[(c * ngL + d) * 64];
+      b_ready = true;
+    }
     if (tid < 64) {
       if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (!broken) {
@@ -680,12 +692,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int u = r; u < U; u += n) {
           const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
           f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
+          const bool pre = b_ready && u == r;
 #pragma unroll
           for (int d = 0; d < DEPTH; ++d) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
 #pragma unroll
-            for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + d) * 64];
+            for (int c = 0; c < 2; ++c) rb_[d][c] = pre ? rbp[d][c] : pb[(c * ngL + d) * 64];
           }
           ServeEpi ep[2];
           f32x4 rv[2], wo[2][NDT];
@@ -758,9 +771,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         }
         if (second) cur = t2;
+        b_ready = false;
       }
       P3D_SERVE_STAMP(tr, 1);
-      group_sync();
+      group_sync(ph + 1);
       P3D_SERVE_STAMP(tr, 2);
     }
     prev_row0 = row0;

@@ -5,10 +5,12 @@
 Modes (BASELINE.json configs):
   infer  (default, configs[1]) L=1024, 2 residual blocks, BN, batch 64, fp32 inference.
          One step = one forward pass over one batch of 64 poses (its own synthetic
-         batch, resident in HBM).  S = 4 streams (one per hardware queue) each replay
-         their own HIP graph of steps over a private workspace slot, so independent
-         batches overlap; every step still runs its own six layer kernels over its own
-         64 rows.  The single-stream rate is reported as "single_stream".
+         batch, resident in HBM).  Headline path: p3d_serve (k_serve), one persistent
+         launch per <= --launch-steps steps; each XCD runs whole batch-64 steps (all six
+         layers of a step on that XCD's CUs, hand-offs in its L2), steps dealt round-robin
+         over the XCDs.  Beside it ("stream_chain"): the per-step kernel chain (six
+         launches per step, p3d_forward_ex), S = 4 streams each replaying a HIP graph of
+         steps over a private workspace slot; its single-stream rate as "single_stream".
   train  (configs[2]) same model, one step = fwd + MSE + bwd + [RCCL all-reduce] +
          TF1 Adam at batch 64 per GPU, keep_prob 0.5.
   eval   (configs[3]) evaluateActionWise sweep over a synthetic 15-action H3.6M-shaped
@@ -231,6 +233,58 @@ def distinct_queue_streams(n, pool=16, cycles=200_000):
     if len(chosen) < n:
         chosen += [c for c in cands if c not in chosen][:n - len(chosen)]
     return chosen
+
+
+def bench_serve(args, rank, world):
+    """K forward steps of one 64-pose batch each through p3d_serve: R persistent launches of
+    K/R steps (<= --launch-steps), every step a batch of 64 of its own (x [K, 64, 32] resident
+    in HBM before the timed region).  Each XCD of the chip runs whole steps -- the six
+    layers of a step on its ~32 CUs, layer hand-offs in its L2 -- and the steps are dealt
+    round-robin over the XCDs; rows never mix across steps (eval BN is per row)."""
+    import torch
+    model, _ = make_model(data_parallel=False, max_batch=BATCH)
+    R = max(1, -(-args.steps // args.launch_steps))
+    while args.steps % R:
+        R += 1
+    C = args.steps // R
+    rng = np.random.default_rng(100 + rank)
+    X = torch.from_numpy(rng.standard_normal((args.steps, BATCH, IN)).astype(np.float32)).cuda()
+    Y = torch.empty((args.steps, BATCH, OUT), dtype=torch.float32, device="cuda")
+    xs = [X[i * C:(i + 1) * C].reshape(C * BATCH, IN) for i in range(R)]
+    ys = [Y[i * C:(i + 1) * C].reshape(C * BATCH, OUT) for i in range(R)]
+
+    def run(k):
+        for i in range(k):
+            model.serve_device(xs[i % R], out=ys[i % R])
+
+    # untimed warmup: the W steps, and at least 3 launches (~20 ms) so the timed launches
+    # run at the clock the chip holds under this load (the first launches ran 5-12 % slower)
+    wl = max(3, -(-args.warmup // C))
+    run(wl)
+    model.serve_check()
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    run(R)
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    model.serve_check()
+    value = world * args.steps * BATCH / dt
+    # dominant (only) kernel, timed live: R launches, each carrying a start/stop event pair
+    # attached to its dispatch (hipExtLaunchKernel), the interval rocprofv3 reports
+    prof = profile_kernels(model, lambda: run(R))
+    cnt, avg_us = prof["serve"][0], prof["serve"][1]
+    flop = float(C * BATCH * flops_per_pose())
+    achieved = flop / (avg_us * 1e-6) / 1e12
+    kname = kernel_name(model, 3)
+    traffic = args.traffic if args.traffic is not None else _committed_traffic(kname)
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "kernel": kname + " (persistent: %d batch-64 steps per launch, whole network per XCD, fp32 MFMA 16x16x4)" % C,
+            "flop_per_launch": int(flop), "steps_per_launch": C, "warmup_launches": wl, "avg_us": round(avg_us, 3),
+            "launches_timed": cnt,
+            "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+    model.close()
+    return value, dt, roof
 
 
 def bench_infer(args, rank, world):
@@ -748,6 +802,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--mode", choices=["infer", "train", "eval", "stress", "data"], default="infer")
     ap.add_argument("--graph-steps", type=int, default=240)
+    ap.add_argument("--launch-steps", type=int, default=1000, help="batch-64 steps per persistent p3d_serve launch")
+    ap.add_argument("--no-streams", action="store_true", help="skip the per-step kernel-chain sub-measurement")
     ap.add_argument("--streams", type=int, default=4, help="independent batch streams (inference)")
     ap.add_argument("--queue-probe", type=int, default=0,
                     help="pick the inference streams by observed hardware-queue concurrency")
@@ -771,10 +827,21 @@ def main():
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     train = single = sweep = api = data = None
+    chain = None
     if args.mode == "infer":
-        value, dt, roof, single = bench_infer(args, rank, world)
-        workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step, "
-                    "%d stream(s)" % args.streams)
+        value, dt, roof = bench_serve(args, rank, world)
+        workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step; "
+                    "p3d_serve persistent launches of %d steps, whole network per XCD"
+                    % roof["steps_per_launch"])
+        if not args.no_streams:   # the per-step kernel chain (six launches per step), 4 streams
+            try:
+                cv, cdt, croof, single = bench_infer(args, rank, world)
+                chain = {"workload": "same steps as six kernel launches each (p3d_forward_ex), %d stream(s) "
+                                     "of HIP graphs" % args.streams,
+                         "value": round(cv, 1), "unit": "poses/s", "ms_per_step": round(1000.0 * cdt / args.steps, 5),
+                         "roofline": croof}
+            except Exception as exc:
+                chain = {"error": repr(exc)[:300]}
         if args.train_steps > 0:   # cfg3 beside the headline, same ranks (data parallel)
             try:
                 tv, tdt, troof, tmode = bench_train(args, rank, world, steps=args.train_steps, warmup=64)
@@ -840,6 +907,8 @@ def main():
                            {"workload": workload, "global_batch": 1024 * world, "linear_size": 4096,
                             "num_layers": 4, "parallelism": "dp%d" % world}),
                 "roofline": roof, "cpu_baseline": cpu}
+        if chain is not None:
+            line["stream_chain"] = chain
         if single is not None:
             line["single_stream"] = single
         if train is not None:
