@@ -215,38 +215,41 @@ __device__ __forceinline__ f32x4 p3d_ring_run(ServeRingA<DEPTH, KS>& RA, ServeRi
 
 // ---- epilogue: lane (j, q) of the tile holds row 16rt + j, columns n0 .. n0+3 ---------
 struct ServeEpi {
-  f32x4 b, inv, shift;
+  f32x4 b, g, be, mu, va;
   float mx;
 };
 
-// Loaded (and the BN factors formed) before the contraction, so neither the loads nor
-// the divides sit between the contraction and the stores.  Same arithmetic as
-// k_gemm_f32's / k_fwd's epilogue: inv = gamma / sqrt(var + eps), shift = beta - mean*inv.
+// Requested before the contraction; the BN factors are formed after it (forming them here
+// would make the wave wait for these loads -- and, vmcnt being in order, for every ring load
+// issued before them -- before its first MFMA: measured +2.2 us per layer).
 __device__ __forceinline__ ServeEpi p3d_epi_load(const ServeLayer& ly, int n0, int bn, float eps) {
+  (void)eps;
   ServeEpi e;
-  e.mx = ly.wsq ? fmaxf(sqrtf(*ly.wsq), 1.0f) : 1.0f;
+  e.mx = ly.wsq ? *ly.wsq : 1.0f;   // ||W||^2 here; maxnorm = max(sqrt(.), 1) in the apply
   e.b = *(const f32x4*)(ly.bias + n0);
-  e.inv = f32x4{1.f, 1.f, 1.f, 1.f};
-  e.shift = f32x4{0.f, 0.f, 0.f, 0.f};
+  e.g = e.be = e.mu = e.va = f32x4{0.f, 0.f, 0.f, 0.f};
   if (bn) {
-    const f32x4 g = *(const f32x4*)(ly.gamma + n0), be = *(const f32x4*)(ly.beta + n0);
-    const f32x4 mu = *(const f32x4*)(ly.mmean + n0), va = *(const f32x4*)(ly.mvar + n0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      e.inv[k] = (1.0f / sqrtf(va[k] + eps)) * g[k];
-      e.shift[k] = be[k] - mu[k] * e.inv[k];
-    }
+    e.g = *(const f32x4*)(ly.gamma + n0); e.be = *(const f32x4*)(ly.beta + n0);
+    e.mu = *(const f32x4*)(ly.mmean + n0); e.va = *(const f32x4*)(ly.mvar + n0);
   }
   return e;
 }
 
-// z = acc / maxnorm + b; y = relu(z * inv + shift)
-__device__ __forceinline__ f32x4 p3d_epi_apply(const ServeEpi& ep, f32x4 acc, bool wsq, int bn) {
+// Same arithmetic as k_gemm_f32's / k_fwd's epilogue: z = acc / maxnorm + b;
+// y = relu(z * inv + (beta - mean * inv)), inv = gamma / sqrt(var + eps).
+__device__ __forceinline__ f32x4 p3d_epi_apply(const ServeEpi& ep, f32x4 acc, bool wsq, int bn, float eps) {
   f32x4 o;
+  const float mx = fmaxf(sqrtf(ep.mx), 1.0f);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const float z = (wsq ? acc[e] / ep.mx : acc[e]) + ep.b[e];
-    o[e] = fmaxf(bn ? z * ep.inv[e] + ep.shift[e] : z, 0.0f);
+    const float z = (wsq ? acc[e] / mx : acc[e]) + ep.b[e];
+    if (bn) {
+      const float inv = (1.0f / sqrtf(ep.va[e] + eps)) * ep.g[e];
+      const float shift = ep.be[e] - ep.mu[e] * inv;
+      o[e] = fmaxf(z * inv + shift, 0.0f);
+    } else {
+      o[e] = fmaxf(z, 0.0f);
+    }
   }
   return o;
 }
@@ -369,7 +372,7 @@ __device__ P3D_SERVE_P0_ATTR void p3d_serve_phase0(const ServeArgs& p, int r, in
       if (g < ngK0)
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[g][e], xa[g][e], acc, 0, 0, 0);
-    const f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn);
+    const f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn, p.eps);
     if (lastp) p3d_serve_partial<NDT>(wo, yv, rt, ct, xch, pdst + (int64_t)u * PT);
     else *(f32x4*)(act + ((int64_t)(rt * ngL + ctg) * 64 + lane) * 4) = yv;
   }
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
             if (res) rv = p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4));
             if (lastp) p3d_wo_load<NDT>(lo, ctg, ngL, wo);
           }
-          f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn);
+          f32x4 yv = p3d_epi_apply(ep, acc, wsq_any, p.bn, p.eps);
           if (res) yv += rv;
           if (lastp) p3d_serve_partial<NDT>(wo, yv, rt, ct, xch, pdst + (int64_t)u * PT);
           else *(f32x4*)(Y + off) = yv;
@@ -672,7 +675,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
               if (g < ngK0)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[c][g][e], xa[g][e], acc, 0, 0, 0);
-            yv[c] = p3d_epi_apply(ep[c], acc, wsq_any, p.bn);
+            yv[c] = p3d_epi_apply(ep[c], acc, wsq_any, p.bn, p.eps);
           }
           if (lastp) partial(yv, wo, pdst + (int64_t)u * PT);
           else {
@@ -715,7 +718,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #ifdef P3D_TRACE
-          if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memtime();
+          if (tr && tid == 0) tr[5] = wall_clock64();   // prologue requested
+          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime();
 #endif
           for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
 #pragma unroll
@@ -727,6 +731,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
                   for (int t = 0; t < 4; ++t)
                     acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+#ifdef P3D_TRACE
+              if (tr && tid == 0 && g0 == 0 && d == 0) tr[7] = wall_clock64();   // first k-group issued
+#endif
               const int gn = g0 + DEPTH + d;
 #pragma unroll
               for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + P3D_SERVE_DIAG_A(gn) * 1024);
@@ -746,7 +753,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                   acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
           P3D_SERVE_STAMP(tr, 3);
 #ifdef P3D_TRACE
-          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime();
+          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime() - tr[6];   // loop shader cycles
 #endif
 #pragma unroll
           for (int c = 0; c < 2; ++c)
@@ -760,7 +767,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             f32x4 sacc = red[(w * 2 + c) * 64 + lane];   // slice 0, tile (w, c)
 #pragma unroll
             for (int k = 1; k < 4; ++k) sacc += red[(k * 8 + w * 2 + c) * 64 + lane];
-            yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn);
+            yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn, p.eps);
             if (res) yv[c] += rv[c];
           }
           __syncthreads();

@@ -111,8 +111,10 @@ int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t tr
  * keep_prob 1; x [B, input_size], y [B, output_size] device pointers.  fp32 models with
  * linear_size % 128 == 0, input_size <= 64, output_size <= 64, at most 7 blocks.
  * Results equal p3d_forward's to fp32 rounding (the output layer sums 32-column partials
- * in fixed order; deterministic).  Returns P3D_ERR_HIP if the device never ran every
- * workgroup of the launch together (reported by the next p3d_serve_check). */
+ * in fixed order; deterministic).  The launch is one workgroup per CU and needs all of
+ * them resident together: do not run two p3d_serve launches concurrently on one device
+ * (other kernels merely delay it).  A launch whose workgroups could not all synchronise
+ * stops within ~0.5 s and is reported by the next p3d_serve_check (P3D_ERR_HIP). */
 int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
 /* 0 if every p3d_serve launch so far completed its synchronisation (device read; syncs). */
 int p3d_serve_check(p3d_model* m);

@@ -55,12 +55,17 @@ def main():
               (rr, float(np.mean(step)) if step else 0.0))
         for ph in range(P):
             print("   phase %d: %s" % (ph, np.round(acc[ph], 2)))
-        # k_serve4 stamps s_memtime (shader clock) around the contraction: effective clock
-        cyc = [t[x_, jl, ph, 6] - t[x_, jl, ph, 5] for x_ in range(8) for jl in range(2, 8) for ph in range(1, P)
-               if t[x_, jl, ph, 6] > t[x_, jl, ph, 5] > 0]
-        if cyc:
-            print("   contraction: %.0f shader cycles -> %.2f GHz over the measured %.2f us" %
-                  (np.mean(cyc), np.mean(cyc) / (np.mean(acc[1:, 0]) * 1e3), np.mean(acc[1:, 0])))
+        # k_serve4 stamps: 5 = prologue requested, 7 = first k-group's MFMAs issued (its
+        # operands arrived), 3 = contraction done; 6 = shader cycles of the ring loop
+        sub = [(t[x_, jl, ph, 5] - t[x_, jl, ph, 0], t[x_, jl, ph, 7] - t[x_, jl, ph, 5],
+                t[x_, jl, ph, 3] - t[x_, jl, ph, 7], t[x_, jl, ph, 6])
+               for x_ in range(8) for jl in range(2, 8) for ph in range(1, P)
+               if t[x_, jl, ph, 7] > t[x_, jl, ph, 5] > 0]
+        if sub:
+            a = np.mean(np.array(sub, dtype=np.float64), axis=0)
+            print("   hidden contraction: prologue %.2f us, first fragments %.2f us, loop %.2f us "
+                  "(%.0f shader cycles -> %.2f GHz)" % (a[0] / 100, a[1] / 100, a[2] / 100, a[3],
+                                                        a[3] / ((a[1] + a[2]) / 100) / 1e3))
     m.close()
 
 
