@@ -1191,7 +1191,8 @@ struct p3d_model {
   int serve_groups = 8;     // XCD groups that take steps (env P3D_SERVE_GROUPS)
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
-  int serve_w4 = 1;         // 1: k_serve4 (4-wave workgroups, 512 registers per wave; env P3D_SERVE_W4)
+  int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (pipelined steps), 1 = k_serve4
+                            // (4-wave workgroups, 512 registers per wave), 0 = k_serve (8-wave); N = 0: k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -1866,8 +1867,7 @@ extern "C" int p3d_forward(p3d_model* m, const float* x, int64_t B, float* y, in
 static int serve_depth_for(const p3d_model* m, int L, int ks) {
   const int ng = L / 16 / ks;
   int d = m->serve_depth;
-  if (d != 1 && d != 2 && d != 3 && d != 4 && d != 8) d = 2;
-  if (d > 4 && !m->serve_w4) d = 4;
+  if (d != 1 && d != 2 && d != 3 && d != 4) d = 2;
   if (d == 3 && m->serve_w4) d = 2;
   while (d > 1 && ng % d != 0) --d;
   return d;
@@ -1875,10 +1875,16 @@ static int serve_depth_for(const p3d_model* m, int L, int ks) {
 
 template <int NDT>
 static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
-  if (m->serve_w4) {   // 4-wave workgroups, one wave per SIMD (k_serve4); K slices of ngL/4 k-groups
+  if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: k_serve4 + steps software-pipelined
     const int d = serve_depth_for(m, a.L, 4);
-    if (d == 8) go(ps, k_serve4<8, NDT>, dim3(grid), dim3(256), st, a);
-    else if (d == 4) go(ps, k_serve4<4, NDT>, dim3(grid), dim3(256), st, a);
+    if (d == 4) go(ps, k_serve5<4, NDT>, dim3(grid), dim3(256), st, a);
+    else if (d == 2) go(ps, k_serve5<2, NDT>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_serve5<1, NDT>, dim3(grid), dim3(256), st, a);
+    return;
+  }
+  if (m->serve_w4 && a.nblk > 0) {   // 4-wave workgroups, one wave per SIMD (k_serve4); K slices of ngL/4 k-groups
+    const int d = serve_depth_for(m, a.L, 4);
+    if (d == 4) go(ps, k_serve4<4, NDT>, dim3(grid), dim3(256), st, a);
     else if (d == 2) go(ps, k_serve4<2, NDT>, dim3(grid), dim3(256), st, a);
     else go(ps, k_serve4<1, NDT>, dim3(grid), dim3(256), st, a);
     return;
@@ -2314,8 +2320,9 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
   } else if (what == 3) {
     const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
-    if (m->serve_w4)
-      n = "k_serve4<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ">";
+    if (m->serve_w4 && m->cfg.num_layers > 0)
+      n = std::string(m->serve_w4 == 5 ? "k_serve5<" : "k_serve4<") +
+          std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ">";
     else
       n = "k_serve<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, ks)) + ", " + std::to_string(ndt) + ", " +
           std::to_string(ks) + ">";

@@ -294,26 +294,13 @@ __device__ __forceinline__ void p3d_serve_partial(const f32x4 (&wo)[NDT], f32x4 
 // Output of one step from its partials: y[row, col] = (sum_u part[u]) / maxnorm + b4.
 // Partial element e4 = (tile (rt, o), lane (i, q)) holds rows 16rt + 4q + r, column 16o + i.
 // This workgroup handles its share [r/n, (r+1)/n) of the float4 elements.
+// y[row, col] = sum / maxnorm + b4 for partial element e4 of the step at row0
 template <int NDT>
-__device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const ServeLayer& lo, const float* pb, int U,
-                                                 int64_t row0, int r, int n) {
-  constexpr int E4 = 4 * NDT * 64;
-  const int s = (int)(((int64_t)E4 * r) / n), e = (int)(((int64_t)E4 * (r + 1)) / n);
-  const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
-  for (int e4 = s + (int)threadIdx.x; e4 < e; e4 += (int)blockDim.x) {
-  f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-  int u = 0;
-  for (; u + 8 <= U; u += 8) {
-    f32x4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = p3d_ld_sc1(rs, ((u + k) * E4 + e4) * 16);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sum += v[k];
-  }
-  for (; u < U; ++u) sum += p3d_ld_sc1(rs, (u * E4 + e4) * 16);
+__device__ __forceinline__ void p3d_serve_store_out(const ServeArgs& p, const ServeLayer& lo, f32x4 sum, int e4,
+                                                    int64_t row0) {
   const int tile = e4 >> 6, ln = e4 & 63, rt = tile / NDT, o = tile % NDT;
   const int col = 16 * o + (ln & 15), q = ln >> 4;
-  if (col >= p.ND) continue;
+  if (col >= p.ND) return;
   const float mx = lo.wsq ? fmaxf(sqrtf(*lo.wsq), 1.0f) : 1.0f;
   const float bb = lo.bias[col];
 #pragma unroll
@@ -321,6 +308,27 @@ __device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const Serve
     const int64_t row = row0 + 16 * rt + 4 * q + k;
     if (row < p.M) p.y[row * p.ND + col] = (lo.wsq ? sum[k] / mx : sum[k]) + bb;
   }
+}
+
+// The units' partials of one element are summed as 8 consecutive slices (slice sums in unit
+// order, then the slices in order) -- the association k_serve5's split reduction uses, so
+// every path gives the same bits.  This workgroup handles elements [E4*r/n, E4*(r+1)/n).
+template <int NDT>
+__device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const ServeLayer& lo, const float* pb, int U,
+                                                 int64_t row0, int r, int n) {
+  constexpr int E4 = 4 * NDT * 64;
+  const int s = (int)(((int64_t)E4 * r) / n), e = (int)(((int64_t)E4 * (r + 1)) / n);
+  const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
+  for (int e4 = s + (int)threadIdx.x; e4 < e; e4 += (int)blockDim.x) {
+    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < 8; ++sl) {
+      const int ub = (U * sl) >> 3, ue = (U * (sl + 1)) >> 3;
+      if (ub == ue) continue;
+      f32x4 ss = p3d_ld_sc1(rs, (ub * E4 + e4) * 16);
+      for (int u = ub + 1; u < ue; ++u) ss += p3d_ld_sc1(rs, (u * E4 + e4) * 16);
+      sum += ss;
+    }
+    p3d_serve_store_out<NDT>(p, lo, sum, e4, row0);
   }
 }
 
@@ -785,6 +793,313 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       P3D_SERVE_STAMP(tr, 2);
     }
     prev_row0 = row0;
+  }
+  if (prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
+}
+
+// =====================================================================================
+// k_serve5: k_serve4's workgroups and contraction, with the steps of a group software-
+// pipelined so a step costs only its 2N hidden-layer phases:
+//   * the input layer of step b+1 (it depends on nothing of step b) runs in the last
+//     hidden phase of step b, after that phase's contraction, into the activation buffer
+//     that phase does not touch (buffer rotation c0' = c0 + 2N mod 3); only the group's
+//     first step has an input-layer phase of its own;
+//   * the output of step b (the sum of its 32 fused output-layer partials) is formed in
+//     the first hidden phase of step b+1, after its contraction (split over the workgroup:
+//     8 unit slices x 32 elements, combined in LDS in slice order);
+//   * every off-contraction load (the next layer's first weight fragments, the next step's
+//     inputs and layer-0 operands, the partials) is requested right after the contraction,
+//     so its latency hides under the K-combine and the epilogue.
+// Needs N >= 1 block (N = 0 runs k_serve).
+// =====================================================================================
+template <int DEPTH, int NDT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve5(ServeArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 8 * 64];     // [slice][rt*2 + ct][lane] (32 KB)
+  __shared__ __attribute__((aligned(16))) f32x4 rsum[8 * 32];        // split output reduction (4 KB)
+  __shared__ int sh[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
+  const int q4 = 4 * (lane >> 4);
+
+  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
+  if (tid == 0) {
+    unsigned xr;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+    const int xcc = (int)(xr & 7u);
+    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int bad = 0, spin = 0;
+    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
+    }
+    sh[0] = xcc; sh[1] = (int)rank;
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[2] = bad;
+  }
+  __syncthreads();
+  if (sh[2]) return;
+  const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
+  int ng = 0, gi = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+    if (sh[8 + x] > 0) { if (x == xcc) gi = ng; ++ng; }
+  if (p.max_groups > 0 && ng > p.max_groups) {
+    ng = p.max_groups;
+    if (gi >= ng) gi = p.nb;   // this group takes no steps
+  }
+  unsigned* flags = p.sync + 64 + 64 * xcc;
+  const int64_t slab = (int64_t)64 * L;
+  float* act = p.act + (int64_t)xcc * 3 * slab;
+  constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
+  constexpr int E4 = 4 * NDT * 64;           // float4 elements of a step's output partial
+  float* part = p.part + (int64_t)xcc * 2 * U * PT;
+  const ServeLayer& li = p.ly[0];
+  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
+  const bool wsq_any = li.wsq != nullptr;    // max-norm is all layers or none
+  const int NH = 2 * p.nblk;                 // hidden layers = phases per step
+  unsigned nsync = 0;
+  bool broken = false;
+  const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
+  // this workgroup's share of a step's output elements, split over (slice, element) threads
+  const int es = (int)(((int64_t)E4 * r) / n), ecnt = (int)(((int64_t)E4 * (r + 1)) / n) - es;
+  const bool split_red = r < U && ecnt <= 32 && U <= 64;
+  const int rsl = tid >> 5, rei = tid & 31;
+
+  auto group_sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++nsync;
+    if (tid < 64) {
+      if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!broken) {
+        int spin = 0;
+        while (true) {
+          const unsigned v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : nsync;
+          if (__all(v >= nsync)) break;
+          if (++spin > P3D_SERVE_SPIN) {
+            broken = true;
+            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  // input layer of unit u for the step at row rbase into act buffer cbuf (row tile w, both
+  // column tiles); operands as loaded by in_load
+  struct InOps { f32x4 xa[4], wb[2][4]; ServeEpi ep[2]; };
+  auto in_load = [&](int u, int64_t rbase, InOps& o) {
+    int64_t rowc = rbase + 16 * w + (lane & 15);
+    rowc = rowc < p.M ? rowc : p.M - 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g < ngK0) {
+        o.xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          o.wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
+      }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) o.ep[c] = p3d_epi_load(li, 16 * (2 * u + c) + q4, p.bn, p.eps);
+  };
+  auto in_finish = [&](int u, const InOps& o, int cbuf) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (g < ngK0)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o.wb[c][g][e], o.xa[g][e], acc, 0, 0, 0);
+      *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) =
+          p3d_epi_apply(o.ep[c], acc, wsq_any, p.bn, p.eps);
+    }
+  };
+
+  f32x4 rbp[DEPTH][2];                       // next layer's first weight fragments
+  bool b_ready = false;
+  auto b_prefetch = [&](int layer) {
+    if (r >= U) return;
+    const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * r) * ngL + gb) * 64 + lane;
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) rbp[d][c] = pbn[(c * ngL + d) * 64];
+    b_ready = true;
+  };
+
+  int jl = 0, c0 = 0;
+  int64_t prev_row0 = -1;
+  if (gi < p.nb) {                           // the group's first step: its input layer alone
+    for (int u = r; u < U; u += n) {
+      InOps o;
+      in_load(u, (int64_t)gi * 64, o);
+      in_finish(u, o, 0);
+    }
+    b_prefetch(1);
+    group_sync();
+  }
+  for (int b = gi; b < p.nb; b += ng, ++jl) {
+    const int64_t row0 = (int64_t)b * 64;
+    const bool has_next = b + ng < p.nb;
+    const int c0n = (c0 + 2 * p.nblk) % 3;   // buffer the next step's input layer writes
+    int cur = c0;
+    float* pdst = part + (int64_t)(jl & 1) * U * PT;
+    const float* prev_part = part + (int64_t)((jl - 1) & 1) * U * PT;
+    for (int ph = 1; ph <= NH; ++ph) {
+      unsigned long long* tr = P3D_SERVE_TR(xcc, r, jl, ph);
+      P3D_SERVE_STAMP(tr, 0);
+      const bool lastp = (ph == NH);
+      const bool red_here = (ph == 1 && prev_row0 >= 0);
+      if (red_here && !split_red) p3d_serve_reduce<NDT>(p, lo, prev_part, U, prev_row0, r, n);
+      const ServeLayer& ly = p.ly[ph];
+      const bool second = ((ph - 1) & 1) == 1;
+      const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
+      const float* A = act + (second ? t1 : cur) * slab;
+      float* Y = act + (second ? t2 : t1) * slab;
+      const float* res = (second && p.residual) ? act + cur * slab : nullptr;
+      const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
+      const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
+      for (int u = r; u < U; u += n) {
+        const bool first_u = (u == r);
+        const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
+        f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
+        const bool pre = b_ready && first_u;
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) rb_[d][c] = pre ? rbp[d][c] : pb[(c * ngL + d) * 64];
+        }
+        b_ready = false;
+        ServeEpi ep[2];
+        f32x4 rv[2], wo[2][NDT];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int64_t off = ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4;
+          ep[c] = p3d_epi_load(ly, 16 * (2 * u + c) + q4, p.bn, p.eps);
+          rv[c] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
+        }
+        f32x4 acc[2][4];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
+#pragma unroll
+          for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                  acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+            const int gn = g0 + DEPTH + d;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + gn * 1024);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + gn) * 64];
+            __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+        P3D_SERVE_STAMP(tr, 3);
+        // ---- off-contraction loads, their latency under the combine and epilogue ----------
+        __builtin_amdgcn_sched_barrier(0);
+        if (first_u) {
+          if (!lastp) b_prefetch(ph + 1);
+          else if (has_next) b_prefetch(1);
+        }
+        f32x4 rpv[8];
+        const bool red_now = red_here && split_red && first_u && rei < ecnt;
+        if (red_now) {
+          const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(prev_part);
+          const int ub = (U * rsl) >> 3, ue = (U * (rsl + 1)) >> 3;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
+        }
+        InOps nx;
+        const bool in_now = lastp && has_next;   // the next step's input layer, this unit
+        if (in_now) in_load(u, row0 + (int64_t)ng * 64, nx);
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- K-slice combine (LDS), epilogue ----------------------------------------------
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) red[(w * 8 + t * 2 + c) * 64 + lane] = acc[c][t];
+        if (red_here && split_red && first_u) {
+          f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (red_now) {
+            const int ub = (U * rsl) >> 3, ue = (U * (rsl + 1)) >> 3;
+            if (ub < ue) ss = rpv[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k)
+              if (ub + k < ue) ss += rpv[k];
+          }
+          rsum[rsl * 32 + rei] = ss;
+        }
+        __syncthreads();
+        P3D_SERVE_STAMP(tr, 4);
+        if (red_here && split_red && first_u && tid < ecnt) {
+          f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int sl = 0; sl < 8; ++sl) tot += rsum[sl * 32 + tid];
+          p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
+        }
+        f32x4 yv[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          f32x4 sacc = red[(w * 2 + c) * 64 + lane];   // slice 0, tile (w, c)
+#pragma unroll
+          for (int k = 1; k < 4; ++k) sacc += red[(k * 8 + w * 2 + c) * 64 + lane];
+          yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn, p.eps);
+          if (res) yv[c] += rv[c];
+        }
+        if (lastp) {
+#pragma unroll
+          for (int o = 0; o < NDT; ++o) {
+            f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[c][e], wo[c][o][e], pacc, 0, 0, 0);
+            *(f32x4*)(pdst + (int64_t)u * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
+        }
+        if (in_now) in_finish(u, nx, c0n);
+        __syncthreads();   // red / rsum reuse by the next unit
+      }
+      if (second) cur = t2;
+      P3D_SERVE_STAMP(tr, 1);
+      group_sync();
+      P3D_SERVE_STAMP(tr, 2);
+    }
+    prev_row0 = row0;
+    c0 = c0n;
   }
   if (prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
 }
