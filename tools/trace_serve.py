@@ -39,9 +39,11 @@ def main():
         acc = np.zeros((P, 4)); cnt = 0
         for x_ in range(8):
             for jl in range(2, 8):
-                if t[x_, jl, 0, 0] == 0:
+                if t[x_, jl, 0, 0] == 0 and t[x_, jl, 1, 0] == 0:
                     continue
                 for ph in range(P):
+                    if t[x_, jl, ph, 0] == 0:   # k_serve5 has no phase 0
+                        continue
                     b, c, w, k3, k4 = (t[x_, jl, ph, k] for k in (0, 1, 2, 3, 4))
                     if ph == 0 or k3 == 0:
                         acc[ph] += (c - b, 0, 0, w - c)
@@ -49,8 +51,9 @@ def main():
                         acc[ph] += (k3 - b, k4 - k3, c - k4, w - c)
                 cnt += 1
         acc /= max(cnt, 1) * 100.0
-        step = [(t[x_, jl + 1, 0, 0] - t[x_, jl, 0, 0]) / 100.0 for x_ in range(8) for jl in range(2, 7)
-                if t[x_, jl + 1, 0, 0]]
+        f0 = 0 if t[:, :, 0, 0].any() else 1
+        step = [(t[x_, jl + 1, f0, 0] - t[x_, jl, f0, 0]) / 100.0 for x_ in range(8) for jl in range(2, 7)
+                if t[x_, jl + 1, f0, 0] and t[x_, jl, f0, 0]]
         print("rank %d: step %.2f us; per phase [contraction, K-combine, epilogue, barrier] us:" %
               (rr, float(np.mean(step)) if step else 0.0))
         for ph in range(P):
