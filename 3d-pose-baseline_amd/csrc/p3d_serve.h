@@ -40,6 +40,9 @@
 #define P3D_SERVE_MAXL 16          // input + 2*blocks + output layers
 #define P3D_SERVE_SYNC_WORDS 640   // [0..7] census, [8] arrivals, [64 + 64*x + r] flag of member r of group x
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
+#ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
+#define P3D_SERVE_SLICE_WAIT 1
+#endif
 #ifndef P3D_SERVE_PREFETCH_B       // request the next layer's weight fragments inside the barrier
 #define P3D_SERVE_PREFETCH_B 1
 #endif
@@ -871,27 +874,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool split_red = r < U && ecnt <= 32 && U <= 64;
   const int rsl = tid >> 5, rei = tid & 31;
 
-  auto group_sync = [&]() {
+  // Group barrier: drain, one lane publishes this member's phase, then every wave waits only
+  // for the members whose output its next contraction reads -- its K slice [gb, gb+gcount)
+  // is units [gb/2, (gb+gcount)/2), unit u produced by member u % n -- or for all members
+  // (full).  A wave loads another member's bytes only after its own poll has matched them.
+  // Write-after-read safety needs no more: a member writes its phase-p output only after its
+  // K-combine barrier, i.e. after all four of its waves saw every member finish phase p-1, so
+  // every read of the buffer being overwritten (last read in phase p-2 or earlier) is done.
+  auto group_sync = [&](bool full) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     ++nsync;
-    if (tid < 64) {
-      if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (!broken) {
-        int spin = 0;
-        while (true) {
-          const unsigned v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    if (tid == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!P3D_SERVE_SLICE_WAIT) full = true;
+    const int cnt = full ? n : (gcount >> 1), ub = gb >> 1;
+    if (!broken) {
+      int spin = 0;
+      while (true) {
+        const int mem = full ? lane : (ub + lane) % n;
+        const unsigned v = lane < cnt ? __hip_atomic_load(flags + mem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : nsync;
-          if (__all(v >= nsync)) break;
-          if (++spin > P3D_SERVE_SPIN) {
-            broken = true;
-            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
+        if (__all(v >= nsync)) break;
+        if (++spin > P3D_SERVE_SPIN) {
+          broken = true;
+          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
         }
       }
     }
-    __syncthreads();
   };
 
   // input layer of unit u for the step at row rbase into act buffer cbuf (row tile w, both
@@ -946,7 +956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       in_finish(u, o, 0);
     }
     b_prefetch(1);
-    group_sync();
+    group_sync(false);
   }
   for (int b = gi; b < p.nb; b += ng, ++jl) {
     const int64_t row0 = (int64_t)b * 64;
@@ -1095,7 +1105,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       if (second) cur = t2;
       P3D_SERVE_STAMP(tr, 1);
-      group_sync();
+      // after a step's last phase the output reduction (next step's first phase, or the final
+      // one below) reads every unit's partial -- unless split, when each wave reads exactly
+      // its producers' partials
+      group_sync(lastp && (!has_next || !split_red));
       P3D_SERVE_STAMP(tr, 2);
     }
     prev_row0 = row0;
