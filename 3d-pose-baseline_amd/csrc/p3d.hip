@@ -1188,9 +1188,10 @@ struct p3d_model {
   unsigned* serve_sync = nullptr;
   int* serve_err = nullptr;
   int serve_grid = 0;
-  int serve_groups = 8;     // XCD groups that take steps (env P3D_SERVE_GROUPS)
+  int serve_groups = 0;     // at most this many groups take steps, 0 = all (env P3D_SERVE_GROUPS)
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
+  int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (pipelined steps), 1 = k_serve4
                             // (4-wave workgroups, 512 registers per wave), 0 = k_serve (8-wave); N = 0: k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -1416,6 +1417,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_KS")) m->serve_ks = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_W4")) m->serve_w4 = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_SPLIT")) m->serve_split = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   {
     StepState s0{};
@@ -1877,9 +1879,16 @@ template <int NDT>
 static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
   if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: k_serve4 + steps software-pipelined
     const int d = serve_depth_for(m, a.L, 4);
-    if (d == 4) go(ps, k_serve5<4, NDT>, dim3(grid), dim3(256), st, a);
-    else if (d == 2) go(ps, k_serve5<2, NDT>, dim3(grid), dim3(256), st, a);
-    else go(ps, k_serve5<1, NDT>, dim3(grid), dim3(256), st, a);
+    if (m->serve_split == 4) {
+      if (d == 2) go(ps, k_serve5<2, NDT, 4>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 4>, dim3(grid), dim3(256), st, a);
+    } else if (m->serve_split == 2) {
+      if (d == 2) go(ps, k_serve5<2, NDT, 2>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 2>, dim3(grid), dim3(256), st, a);
+    } else {
+      if (d == 2) go(ps, k_serve5<2, NDT, 1>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 1>, dim3(grid), dim3(256), st, a);
+    }
     return;
   }
   if (m->serve_w4 && a.nblk > 0) {   // 4-wave workgroups, one wave per SIMD (k_serve4); K slices of ngL/4 k-groups
@@ -1923,7 +1932,7 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     m->serve_grid = cus;   // one 512-thread workgroup per CU (the LDS ring admits one)
-    const int64_t nbuf = 8 * 3 * slab + 8 * 2 * (int64_t)U * PT;
+    const int64_t nbuf = P3D_SERVE_GROUPS * 3 * slab + P3D_SERVE_GROUPS * 2 * (int64_t)U * PT;
     if ((e = hipMalloc(&m->serve_buf, nbuf * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     if ((e = hipMemset(m->serve_buf, 0, nbuf * sizeof(float))) != hipSuccess)
@@ -1938,7 +1947,7 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);
   a.L = L; a.K0 = c.input_size; a.ND = c.output_size; a.nblk = c.num_layers;
   a.bn = c.batch_norm; a.residual = c.residual; a.eps = c.bn_eps;
-  a.act = m->serve_buf; a.part = m->serve_buf + 8 * 3 * slab;
+  a.act = m->serve_buf; a.part = m->serve_buf + P3D_SERVE_GROUPS * 3 * slab;
   a.sync = m->serve_sync; a.err = m->serve_err;
   a.max_groups = m->serve_groups;
   for (size_t l = 0; l < m->layers.size(); ++l) {
@@ -2322,7 +2331,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
     if (m->serve_w4 && m->cfg.num_layers > 0)
       n = std::string(m->serve_w4 == 5 ? "k_serve5<" : "k_serve4<") +
-          std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ">";
+          std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) +
+          (m->serve_w4 == 5 ? ", " + std::to_string(m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1) : std::string("")) + ">";
     else
       n = "k_serve<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, ks)) + ", " + std::to_string(ndt) + ", " +
           std::to_string(ks) + ">";

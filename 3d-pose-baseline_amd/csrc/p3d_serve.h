@@ -38,7 +38,8 @@
 #include "p3d_kernels.h"
 
 #define P3D_SERVE_MAXL 16          // input + 2*blocks + output layers
-#define P3D_SERVE_SYNC_WORDS 640   // [0..7] census, [8] arrivals, [64 + 64*x + r] flag of member r of group x
+#define P3D_SERVE_SYNC_WORDS 2112  // [0..7] census, [8] arrivals, [64 + 64*g + r] flag of member r of group g
+#define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
 #define P3D_SERVE_SLICE_WAIT 1
@@ -313,9 +314,10 @@ __device__ __forceinline__ void p3d_serve_store_out(const ServeArgs& p, const Se
   }
 }
 
-// The units' partials of one element are summed as 8 consecutive slices (slice sums in unit
-// order, then the slices in order) -- the association k_serve5's split reduction uses, so
-// every path gives the same bits.  This workgroup handles elements [E4*r/n, E4*(r+1)/n).
+// The units' partials of one element are summed as 4 consecutive slices (slice sums in unit
+// order, then the slices in order) -- the association k_serve5's split reduction uses (one
+// slice per wave: exactly the units that wave's producers wrote), so every path gives the
+// same bits.  This workgroup handles elements [E4*r/n, E4*(r+1)/n).
 template <int NDT>
 __device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const ServeLayer& lo, const float* pb, int U,
                                                  int64_t row0, int r, int n) {
@@ -324,8 +326,8 @@ __device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const Serve
   const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
   for (int e4 = s + (int)threadIdx.x; e4 < e; e4 += (int)blockDim.x) {
     f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < 8; ++sl) {
-      const int ub = (U * sl) >> 3, ue = (U * (sl + 1)) >> 3;
+    for (int sl = 0; sl < 4; ++sl) {
+      const int ub = (U * sl) >> 2, ue = (U * (sl + 1)) >> 2;
       if (ub == ue) continue;
       f32x4 ss = p3d_ld_sc1(rs, (ub * E4 + e4) * 16);
       for (int u = ub + 1; u < ue; ++u) ss += p3d_ld_sc1(rs, (u * E4 + e4) * 16);
@@ -815,10 +817,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 //     so its latency hides under the K-combine and the epilogue.
 // Needs N >= 1 block (N = 0 runs k_serve).
 // =====================================================================================
-template <int DEPTH, int NDT>
+// SPLIT = 2 / 4: the members of an XCD form SPLIT groups (by rank mod SPLIT) that run
+// different steps, each with ~32/SPLIT CUs: a layer's contraction takes SPLIT times as long
+// while the per-layer fixed costs (hand-off, operand fill, epilogue) stay, so they weigh less.
+template <int DEPTH, int NDT, int SPLIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve5(ServeArgs p) {
   __shared__ __attribute__((aligned(16))) f32x4 red[4 * 8 * 64];     // [slice][rt*2 + ct][lane] (32 KB)
-  __shared__ __attribute__((aligned(16))) f32x4 rsum[8 * 32];        // split output reduction (4 KB)
+  __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64];        // split output reduction (4 KB)
   __shared__ int sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
@@ -847,21 +852,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   __syncthreads();
   if (sh[2]) return;
-  const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
+  const int xcc = sh[0], rx = sh[1], nx = sh[8 + xcc];
+  const int half = rx % SPLIT;                          // group = (XCD, rank mod SPLIT)
+  const int r = rx / SPLIT;
+  const int n = (nx + SPLIT - 1 - half) / SPLIT;
+  const int gid = xcc * SPLIT + half;
   int ng = 0, gi = 0;
 #pragma unroll
   for (int x = 0; x < 8; ++x)
-    if (sh[8 + x] > 0) { if (x == xcc) gi = ng; ++ng; }
+#pragma unroll
+    for (int h = 0; h < SPLIT; ++h) {
+      const int cnt = (sh[8 + x] + SPLIT - 1 - h) / SPLIT;
+      if (cnt > 0) { if (x == xcc && h == half) gi = ng; ++ng; }
+    }
   if (p.max_groups > 0 && ng > p.max_groups) {
     ng = p.max_groups;
     if (gi >= ng) gi = p.nb;   // this group takes no steps
   }
-  unsigned* flags = p.sync + 64 + 64 * xcc;
+  unsigned* flags = p.sync + 64 + 64 * gid;
   const int64_t slab = (int64_t)64 * L;
-  float* act = p.act + (int64_t)xcc * 3 * slab;
+  float* act = p.act + (int64_t)gid * 3 * slab;
   constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
   constexpr int E4 = 4 * NDT * 64;           // float4 elements of a step's output partial
-  float* part = p.part + (int64_t)xcc * 2 * U * PT;
+  float* part = p.part + (int64_t)gid * 2 * U * PT;
   const ServeLayer& li = p.ly[0];
   const ServeLayer& lo = p.ly[2 * p.nblk + 1];
   const bool wsq_any = li.wsq != nullptr;    // max-norm is all layers or none
@@ -871,8 +884,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
   // this workgroup's share of a step's output elements, split over (slice, element) threads
   const int es = (int)(((int64_t)E4 * r) / n), ecnt = (int)(((int64_t)E4 * (r + 1)) / n) - es;
-  const bool split_red = r < U && ecnt <= 32 && U <= 64;
-  const int rsl = tid >> 5, rei = tid & 31;
+  const bool split_red = r < U && ecnt <= 64 && U <= 64;
+  const int rsl = w, rei = lane;             // slice = this wave's producers' units
 
   // Group barrier: drain, one lane publishes this member's phase, then every wave waits only
   // for the members whose output its next contraction reads -- its K slice [gb, gb+gcount)
@@ -937,9 +950,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   f32x4 rbp[DEPTH][2];                       // next layer's first weight fragments
   bool b_ready = false;
-  auto b_prefetch = [&](int layer) {
-    if (r >= U) return;
-    const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * r) * ngL + gb) * 64 + lane;
+  auto b_prefetch = [&](int layer, int unit) {   // the first weight fragments of the next ring
+    if (unit >= U) return;
+    const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * unit) * ngL + gb) * 64 + lane;
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
@@ -955,7 +968,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       in_load(u, (int64_t)gi * 64, o);
       in_finish(u, o, 0);
     }
-    b_prefetch(1);
+    b_prefetch(1, r);
     group_sync(false);
   }
   for (int b = gi; b < p.nb; b += ng, ++jl) {
@@ -983,7 +996,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const bool first_u = (u == r);
         const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
         f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
-        const bool pre = b_ready && first_u;
+        const bool pre = b_ready;
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
 #pragma unroll
@@ -1036,17 +1049,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         P3D_SERVE_STAMP(tr, 3);
         // ---- off-contraction loads, their latency under the combine and epilogue ----------
         __builtin_amdgcn_sched_barrier(0);
-        if (first_u) {
-          if (!lastp) b_prefetch(ph + 1);
-          else if (has_next) b_prefetch(1);
-        }
-        f32x4 rpv[8];
+        if (u + n < U) b_prefetch(ph, u + n);          // this workgroup's next unit
+        else if (!lastp) b_prefetch(ph + 1, r);         // the next layer's first unit
+        else if (has_next) b_prefetch(1, r);            // the next step's first layer
+        f32x4 rpv[16];
         const bool red_now = red_here && split_red && first_u && rei < ecnt;
         if (red_now) {
           const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(prev_part);
-          const int ub = (U * rsl) >> 3, ue = (U * (rsl + 1)) >> 3;
+          const int ub = (U * rsl) >> 2, ue = (U * (rsl + 1)) >> 2;
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
+          for (int k = 0; k < 16; ++k)
             if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
         }
         InOps nx;
@@ -1061,20 +1073,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (red_here && split_red && first_u) {
           f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
           if (red_now) {
-            const int ub = (U * rsl) >> 3, ue = (U * (rsl + 1)) >> 3;
+            const int ub = (U * rsl) >> 2, ue = (U * (rsl + 1)) >> 2;
             if (ub < ue) ss = rpv[0];
 #pragma unroll
-            for (int k = 1; k < 8; ++k)
+            for (int k = 1; k < 16; ++k)
               if (ub + k < ue) ss += rpv[k];
           }
-          rsum[rsl * 32 + rei] = ss;
+          rsum[rsl * 64 + rei] = ss;
         }
         __syncthreads();
         P3D_SERVE_STAMP(tr, 4);
         if (red_here && split_red && first_u && tid < ecnt) {
           f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int sl = 0; sl < 8; ++sl) tot += rsum[sl * 32 + tid];
+          for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 + tid];
           p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
         }
         f32x4 yv[2];
@@ -1101,7 +1113,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int c = 0; c < 2; ++c) *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
         }
         if (in_now) in_finish(u, nx, c0n);
-        __syncthreads();   // red / rsum reuse by the next unit
+        // red / rsum are rewritten by this workgroup's next unit; after its last unit of the
+        // phase the group barrier's workgroup barrier orders the next phase's writes
+        if (u + n < U) __syncthreads();
       }
       if (second) cur = t2;
       P3D_SERVE_STAMP(tr, 1);
