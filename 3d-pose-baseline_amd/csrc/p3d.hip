@@ -1192,8 +1192,8 @@ struct p3d_model {
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
-  int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (pipelined steps), 1 = k_serve4
-                            // (4-wave workgroups, 512 registers per wave), 0 = k_serve (8-wave); N = 0: k_serve
+  int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
+                            // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
   bool prof = false;
   std::vector<hipEvent_t> ev;
@@ -1877,7 +1877,7 @@ static int serve_depth_for(const p3d_model* m, int L, int ks) {
 
 template <int NDT>
 static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
-  if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: k_serve4 + steps software-pipelined
+  if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: 4-wave workgroups, steps software-pipelined
     const int d = serve_depth_for(m, a.L, 4);
     if (m->serve_split == 4) {
       if (d == 2) go(ps, k_serve5<2, NDT, 4>, dim3(grid), dim3(256), st, a);
@@ -1889,13 +1889,6 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
       if (d == 2) go(ps, k_serve5<2, NDT, 1>, dim3(grid), dim3(256), st, a);
       else go(ps, k_serve5<1, NDT, 1>, dim3(grid), dim3(256), st, a);
     }
-    return;
-  }
-  if (m->serve_w4 && a.nblk > 0) {   // 4-wave workgroups, one wave per SIMD (k_serve4); K slices of ngL/4 k-groups
-    const int d = serve_depth_for(m, a.L, 4);
-    if (d == 4) go(ps, k_serve4<4, NDT>, dim3(grid), dim3(256), st, a);
-    else if (d == 2) go(ps, k_serve4<2, NDT>, dim3(grid), dim3(256), st, a);
-    else go(ps, k_serve4<1, NDT>, dim3(grid), dim3(256), st, a);
     return;
   }
   const int ks = m->serve_ks == 4 ? 4 : 8;
@@ -2329,10 +2322,9 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
   } else if (what == 3) {
     const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
-    if (m->serve_w4 && m->cfg.num_layers > 0)
-      n = std::string(m->serve_w4 == 5 ? "k_serve5<" : "k_serve4<") +
-          std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) +
-          (m->serve_w4 == 5 ? ", " + std::to_string(m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1) : std::string("")) + ">";
+    if (m->serve_w4 == 5 && m->cfg.num_layers > 0)
+      n = "k_serve5<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ", " +
+          std::to_string(m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1) + ">";
     else
       n = "k_serve<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, ks)) + ", " + std::to_string(ndt) + ", " +
           std::to_string(ks) + ">";

@@ -534,277 +534,14 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
 }
 
 // =====================================================================================
-// k_serve4: the same persistent XCD-local schedule with 4-wave (256-thread) workgroups,
-// one wave per SIMD, so every wave has the full 512-entry register file (arch VGPRs +
-// AGPRs).  Wave w owns K slice w of the unit (k-groups [w*ngL/4, (w+1)*ngL/4)) for all
-// 4 row tiles x 2 column tiles: per k-group 4 A + 2 B fragments (each operand byte loaded
-// once per CU: 384 KB per layer at L = 1024) for 32 MFMAs on 8 independent accumulators,
-// with a DEPTH-deep register ring.  After the K-slice combine (LDS, slice order) wave w
-// owns row tile w of both column tiles, so the fused output-layer partial of a row tile
-// needs no exchange.
-// =====================================================================================
-template <int DEPTH, int NDT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve4(ServeArgs p) {
-  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 8 * 64];     // [slice][rt*2 + ct][lane] (32 KB)
-  __shared__ int sh[16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
-  const int q4 = 4 * (lane >> 4);
-
-  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
-  if (tid == 0) {
-    unsigned xr;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
-    const int xcc = (int)(xr & 7u);
-    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int bad = 0, spin = 0;
-    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
-    }
-    sh[0] = xcc; sh[1] = (int)rank;
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
-    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh[2] = bad;
-  }
-  __syncthreads();
-  if (sh[2]) return;
-  const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
-  int ng = 0, gi = 0;
-#pragma unroll
-  for (int x = 0; x < 8; ++x)
-    if (sh[8 + x] > 0) { if (x == xcc) gi = ng; ++ng; }
-  if (p.max_groups > 0 && ng > p.max_groups) {
-    ng = p.max_groups;
-    if (gi >= ng) gi = p.nb;   // this group takes no steps
-  }
-  unsigned* flags = p.sync + 64 + 64 * xcc;
-  const int64_t slab = (int64_t)64 * L;
-  float* act = p.act + (int64_t)xcc * 3 * slab;
-  constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
-  float* part = p.part + (int64_t)xcc * 2 * U * PT;
-  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
-  const bool wsq_any = p.ly[0].wsq != nullptr;   // max-norm is all layers or none
-  const int P = 2 * p.nblk + 1;              // phases per step
-  unsigned nsync = 0;
-  bool broken = false;
-  const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
-
-  // the next layer's first weight fragments (independent of the hand-off) are requested
-  // between the drain and the flag poll, so their latency hides under the barrier
-  f32x4 rbp[DEPTH][2];
-  bool b_ready = false;
-  auto group_sync = [&](int next_ph) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    ++nsync;
-    if (P3D_SERVE_PREFETCH_B && next_ph > 0 && next_ph < P && r < U) {
-      const f32x4* pbn = (const f32x4*)p.ly[next_ph].Wf + ((int64_t)(2 * r) * ngL + gb) * 64 + lane;
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) rbp[d][c] = pbn[(c * ngL + d) * 64];
-      b_ready = true;
-    }
-    if (tid < 64) {
-      if (lane == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (!broken) {
-        int spin = 0;
-        while (true) {
-          const unsigned v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : nsync;
-          if (__all(v >= nsync)) break;
-          if (++spin > P3D_SERVE_SPIN) {
-            broken = true;
-            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-    }
-    __syncthreads();
-  };
-
-  // output-layer partial of row tile w: y[c] (A-fragments of k-groups 2u + c) x W4
-  auto partial = [&](const f32x4 (&yv)[2], const f32x4 (&wo)[2][NDT], float* pd) {
-#pragma unroll
-    for (int o = 0; o < NDT; ++o) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[c][e], wo[c][o][e], acc, 0, 0, 0);
-      *(f32x4*)(pd + ((w * NDT + o) * 64 + lane) * 4) = acc;
-    }
-  };
-
-  int jl = 0;
-  int64_t prev_row0 = -1;
-  for (int b = gi; b < p.nb; b += ng, ++jl) {
-    const int64_t row0 = (int64_t)b * 64;
-    int cur = 0;
-    for (int ph = 0; ph < P; ++ph) {
-      unsigned long long* tr = P3D_SERVE_TR(xcc, r, jl, ph);
-      P3D_SERVE_STAMP(tr, 0);
-      const bool lastp = (ph == P - 1);
-      float* pdst = part + (int64_t)(jl & 1) * U * PT;
-      if (ph == 0) {
-        const ServeLayer& li = p.ly[0];
-        for (int u = r; u < U || u == r; u += n) {
-          const bool has = u < U;
-          f32x4 xa[4], wb[2][4], wo[2][NDT];
-          ServeEpi ep[2];
-          if (has) {
-            int64_t rowc = row0 + 16 * w + (lane & 15);
-            rowc = rowc < p.M ? rowc : p.M - 1;
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-              if (g < ngK0) {
-                xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-                  wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
-              }
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              ep[c] = p3d_epi_load(li, 16 * (2 * u + c) + q4, p.bn, p.eps);
-              if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
-            }
-          }
-          if (u == r && prev_row0 >= 0)
-            p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
-          if (!has) break;
-          f32x4 yv[2];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-              if (g < ngK0)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[c][g][e], xa[g][e], acc, 0, 0, 0);
-            yv[c] = p3d_epi_apply(ep[c], acc, wsq_any, p.bn, p.eps);
-          }
-          if (lastp) partial(yv, wo, pdst + (int64_t)u * PT);
-          else {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) *(f32x4*)(act + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
-          }
-        }
-      } else {
-        const ServeLayer& ly = p.ly[ph];
-        const bool second = ((ph - 1) & 1) == 1;
-        const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
-        const float* A = act + (second ? t1 : cur) * slab;
-        float* Y = act + (second ? t2 : t1) * slab;
-        const float* res = (second && p.residual) ? act + cur * slab : nullptr;
-        const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
-        const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
-        for (int u = r; u < U; u += n) {
-          const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
-          f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
-          const bool pre = b_ready && u == r;
-#pragma unroll
-          for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) rb_[d][c] = pre ? rbp[d][c] : pb[(c * ngL + d) * 64];
-          }
-          ServeEpi ep[2];
-          f32x4 rv[2], wo[2][NDT];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int64_t off = ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4;
-            ep[c] = p3d_epi_load(ly, 16 * (2 * u + c) + q4, p.bn, p.eps);
-            rv[c] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
-            if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
-          }
-          f32x4 acc[2][4];
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef P3D_TRACE
-          if (tr && tid == 0) tr[5] = wall_clock64();   // prologue requested
-          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime();
-#endif
-          for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
-#pragma unroll
-            for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                  for (int t = 0; t < 4; ++t)
-                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
-#ifdef P3D_TRACE
-              if (tr && tid == 0 && g0 == 0 && d == 0) tr[7] = wall_clock64();   // first k-group issued
-#endif
-              const int gn = g0 + DEPTH + d;
-#pragma unroll
-              for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + P3D_SERVE_DIAG_A(gn) * 1024);
-#pragma unroll
-              for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + P3D_SERVE_DIAG_B(gn)) * 64];
-              __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
-            }
-          }
-#pragma unroll
-          for (int d = 0; d < DEPTH; ++d)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                  acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
-          P3D_SERVE_STAMP(tr, 3);
-#ifdef P3D_TRACE
-          if (tr && tid == 0) tr[6] = __builtin_amdgcn_s_memtime() - tr[6];   // loop shader cycles
-#endif
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) red[(w * 8 + t * 2 + c) * 64 + lane] = acc[c][t];
-          __syncthreads();
-          P3D_SERVE_STAMP(tr, 4);
-          f32x4 yv[2];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            f32x4 sacc = red[(w * 2 + c) * 64 + lane];   // slice 0, tile (w, c)
-#pragma unroll
-            for (int k = 1; k < 4; ++k) sacc += red[(k * 8 + w * 2 + c) * 64 + lane];
-            yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn, p.eps);
-            if (res) yv[c] += rv[c];
-          }
-          __syncthreads();
-          if (lastp) partial(yv, wo, pdst + (int64_t)u * PT);
-          else {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
-          }
-        }
-        if (second) cur = t2;
-        b_ready = false;
-      }
-      P3D_SERVE_STAMP(tr, 1);
-      group_sync(ph + 1);
-      P3D_SERVE_STAMP(tr, 2);
-    }
-    prev_row0 = row0;
-  }
-  if (prev_row0 >= 0) p3d_serve_reduce<NDT>(p, lo, part + (int64_t)((jl - 1) & 1) * U * PT, U, prev_row0, r, n);
-}
-
-// =====================================================================================
-// k_serve5: k_serve4's workgroups and contraction, with the steps of a group software-
-// pipelined so a step costs only its 2N hidden-layer phases:
+// k_serve5 (default): 4-wave (256-thread) workgroups, one wave per SIMD, so every wave has
+// the full 512-entry register file (arch VGPRs + AGPRs).  Wave w owns K slice w of a unit
+// (k-groups [w*ngL/4, (w+1)*ngL/4)) for all 4 row tiles x 2 column tiles: per k-group 4 A +
+// 2 B fragments (each operand byte loaded once per CU) for 32 MFMAs on 8 independent
+// accumulators, with a DEPTH-deep register ring.  After the K-slice combine (LDS, slice
+// order) wave w owns row tile w of both column tiles, so the fused output-layer partial of a
+// row tile needs no exchange.  The steps of a group are software-pipelined so a step costs
+// only its 2N hidden-layer phases:
 //   * the input layer of step b+1 (it depends on nothing of step b) runs in the last
 //     hidden phase of step b, after that phase's contraction, into the activation buffer
 //     that phase does not touch (buffer rotation c0' = c0 + 2N mod 3); only the group's
