@@ -1192,6 +1192,7 @@ struct p3d_model {
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
+  int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1 or 2, with SPLIT >= 2)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -1418,6 +1419,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_SERVE_KS")) m->serve_ks = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_W4")) m->serve_w4 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_SPLIT")) m->serve_split = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_UPM")) m->serve_upm = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   {
     StepState s0{};
@@ -1879,15 +1881,20 @@ template <int NDT>
 static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
   if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: 4-wave workgroups, steps software-pipelined
     const int d = serve_depth_for(m, a.L, 4);
+    // paired units (UPM = 2, env P3D_SERVE_UPM) where a group has about U/2 members
+    const bool pair = m->serve_upm == 2 && m->serve_split >= 2;
     if (m->serve_split == 4) {
-      if (d == 2) go(ps, k_serve5<2, NDT, 4>, dim3(grid), dim3(256), st, a);
-      else go(ps, k_serve5<1, NDT, 4>, dim3(grid), dim3(256), st, a);
+      if (pair) go(ps, k_serve5<2, NDT, 4, 2>, dim3(grid), dim3(256), st, a);
+      else if (d == 2) go(ps, k_serve5<2, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
     } else if (m->serve_split == 2) {
-      if (d == 2) go(ps, k_serve5<2, NDT, 2>, dim3(grid), dim3(256), st, a);
-      else go(ps, k_serve5<1, NDT, 2>, dim3(grid), dim3(256), st, a);
+      if (pair && d == 2) go(ps, k_serve5<2, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
+      else if (pair) go(ps, k_serve5<1, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
+      else if (d == 2) go(ps, k_serve5<2, NDT, 2, 1>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 2, 1>, dim3(grid), dim3(256), st, a);
     } else {
-      if (d == 2) go(ps, k_serve5<2, NDT, 1>, dim3(grid), dim3(256), st, a);
-      else go(ps, k_serve5<1, NDT, 1>, dim3(grid), dim3(256), st, a);
+      if (d == 2) go(ps, k_serve5<2, NDT, 1, 1>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve5<1, NDT, 1, 1>, dim3(grid), dim3(256), st, a);
     }
     return;
   }
@@ -2323,8 +2330,13 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
   } else if (what == 3) {
     const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
     if (m->serve_w4 == 5 && m->cfg.num_layers > 0)
-      n = "k_serve5<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, 4)) + ", " + std::to_string(ndt) + ", " +
-          std::to_string(m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1) + ">";
+    {
+      const int sp = m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1;
+      const int upm = (m->serve_upm == 2 && sp >= 2) ? 2 : 1;
+      const int d = (upm == 2 && sp == 4) ? 2 : serve_depth_for(m, m->cfg.linear_size, 4);
+      n = "k_serve5<" + std::to_string(d) + ", " + std::to_string(ndt) + ", " + std::to_string(sp) + ", " +
+          std::to_string(upm) + ">";
+    }
     else
       n = "k_serve<" + std::to_string(serve_depth_for(m, m->cfg.linear_size, ks)) + ", " + std::to_string(ndt) + ", " +
           std::to_string(ks) + ">";

@@ -557,9 +557,14 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
 // SPLIT = 2 / 4: the members of an XCD form SPLIT groups (by rank mod SPLIT) that run
 // different steps, each with ~32/SPLIT CUs: a layer's contraction takes SPLIT times as long
 // while the per-layer fixed costs (hand-off, operand fill, epilogue) stay, so they weigh less.
-template <int DEPTH, int NDT, int SPLIT>
+// UPM = 2: a workgroup runs its two units of a layer (u, u + n) as ONE contraction of 4
+// column tiles: the activation fragments are loaded once for both, one fill, one K-combine
+// and one epilogue per phase.  A pair whose second unit does not exist computes a copy of
+// the first and stores nothing for it.
+template <int DEPTH, int NDT, int SPLIT, int UPM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve5(ServeArgs p) {
-  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 8 * 64];     // [slice][rt*2 + ct][lane] (32 KB)
+  constexpr int NC = 2 * UPM;                // column tiles per contraction
+  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NC * 64]; // [slice][rt][ct][lane] (32 / 64 KB)
   __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64];        // split output reduction (4 KB)
   __shared__ int sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -685,15 +690,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  f32x4 rbp[DEPTH][2];                       // next layer's first weight fragments
+  f32x4 rbp[DEPTH][NC];                      // the next ring's first weight fragments
   bool b_ready = false;
-  auto b_prefetch = [&](int layer, int unit) {   // the first weight fragments of the next ring
+  auto b_prefetch = [&](int layer, int unit) {   // units unit, unit + n (UPM = 2)
     if (unit >= U) return;
-    const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * unit) * ngL + gb) * 64 + lane;
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d)
+    for (int k = 0; k < UPM; ++k) {
+      const int uk = (unit + k * n < U) ? unit + k * n : unit;
+      const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * uk) * ngL + gb) * 64 + lane;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) rbp[d][c] = pbn[(c * ngL + d) * 64];
+      for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) rbp[d][2 * k + c] = pbn[(c * ngL + d) * 64];
+    }
     b_ready = true;
   };
 
@@ -729,48 +738,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const float* res = (second && p.residual) ? act + cur * slab : nullptr;
       const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
       const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
-      for (int u = r; u < U; u += n) {
+      for (int u = r; u < U; u += n * UPM) {
         const bool first_u = (u == r);
-        const f32x4* pb = (const f32x4*)ly.Wf + ((int64_t)(2 * u) * ngL + gb) * 64 + lane;
-        f32x4 ra_[DEPTH][4], rb_[DEPTH][2];
+        int uu[UPM];
+        bool uv[UPM];
+#pragma unroll
+        for (int k = 0; k < UPM; ++k) {
+          uv[k] = (u + k * n < U);
+          uu[k] = uv[k] ? u + k * n : u;
+        }
+        const f32x4* pbk[UPM];
+#pragma unroll
+        for (int k = 0; k < UPM; ++k) pbk[k] = (const f32x4*)ly.Wf + ((int64_t)(2 * uu[k]) * ngL + gb) * 64 + lane;
+        f32x4 ra_[DEPTH][4], rb_[DEPTH][NC];
         const bool pre = b_ready;
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
 #pragma unroll
-          for (int c = 0; c < 2; ++c) rb_[d][c] = pre ? rbp[d][c] : pb[(c * ngL + d) * 64];
+          for (int k = 0; k < UPM; ++k)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rb_[d][2 * k + c] = pre ? rbp[d][2 * k + c] : pbk[k][(c * ngL + d) * 64];
         }
         b_ready = false;
-        ServeEpi ep[2];
-        f32x4 rv[2], wo[2][NDT];
+        ServeEpi ep[NC];
+        f32x4 rv[NC], wo[NC][NDT];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int64_t off = ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4;
-          ep[c] = p3d_epi_load(ly, 16 * (2 * u + c) + q4, p.bn, p.eps);
-          rv[c] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
-          if (lastp) p3d_wo_load<NDT>(lo, 2 * u + c, ngL, wo[c]);
+        for (int cc = 0; cc < NC; ++cc) {
+          const int col_t = 2 * uu[cc >> 1] + (cc & 1);
+          const int64_t off = ((int64_t)(w * ngL + col_t) * 64 + lane) * 4;
+          ep[cc] = p3d_epi_load(ly, 16 * col_t + q4, p.bn, p.eps);
+          rv[cc] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if (lastp) p3d_wo_load<NDT>(lo, col_t, ngL, wo[cc]);
         }
-        f32x4 acc[2][4];
+        f32x4 acc[NC][4];
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int t = 0; t < 4; ++t) acc[cc][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
 #pragma unroll
           for (int d = 0; d < DEPTH; ++d) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-              for (int c = 0; c < 2; ++c)
+              for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
-                  acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+                  acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d][t][e], acc[cc][t], 0, 0, 0);
             const int gn = g0 + DEPTH + d;
 #pragma unroll
             for (int t = 0; t < 4; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + gn * 1024);
 #pragma unroll
-            for (int c = 0; c < 2; ++c) rb_[d][c] = pb[(c * ngL + gn) * 64];
+            for (int k = 0; k < UPM; ++k)
+#pragma unroll
+              for (int c = 0; c < 2; ++c) rb_[d][2 * k + c] = pbk[k][(c * ngL + gn) * 64];
             __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
           }
         }
@@ -779,16 +802,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
+            for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
               for (int t = 0; t < 4; ++t)
-                acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][c][e], ra_[d][t][e], acc[c][t], 0, 0, 0);
+                acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d][t][e], acc[cc][t], 0, 0, 0);
         P3D_SERVE_STAMP(tr, 3);
         // ---- off-contraction loads, their latency under the combine and epilogue ----------
         __builtin_amdgcn_sched_barrier(0);
-        if (u + n < U) b_prefetch(ph, u + n);          // this workgroup's next unit
-        else if (!lastp) b_prefetch(ph + 1, r);         // the next layer's first unit
-        else if (has_next) b_prefetch(1, r);            // the next step's first layer
+        if (u + n * UPM < U) b_prefetch(ph, u + n * UPM);   // this workgroup's next unit(s)
+        else if (!lastp) b_prefetch(ph + 1, r);              // the next layer's first unit(s)
+        else if (has_next) b_prefetch(1, r);                 // the next step's first layer
         f32x4 rpv[16];
         const bool red_now = red_here && split_red && first_u && rei < ecnt;
         if (red_now) {
@@ -798,15 +821,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int k = 0; k < 16; ++k)
             if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
         }
-        InOps nx;
-        const bool in_now = lastp && has_next;   // the next step's input layer, this unit
-        if (in_now) in_load(u, row0 + (int64_t)ng * 64, nx);
         __builtin_amdgcn_sched_barrier(0);
         // ---- K-slice combine (LDS), epilogue ----------------------------------------------
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) red[(w * 8 + t * 2 + c) * 64 + lane] = acc[c][t];
+          for (int t = 0; t < 4; ++t) red[((w * 4 + t) * NC + cc) * 64 + lane] = acc[cc][t];
         if (red_here && split_red && first_u) {
           f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
           if (red_now) {
@@ -826,33 +846,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 + tid];
           p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
         }
-        f32x4 yv[2];
+        f32x4 yv[NC];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          f32x4 sacc = red[(w * 2 + c) * 64 + lane];   // slice 0, tile (w, c)
+        for (int cc = 0; cc < NC; ++cc) {
+          f32x4 sacc = red[((0 * 4 + w) * NC + cc) * 64 + lane];   // slice 0, tile (w, cc)
 #pragma unroll
-          for (int k = 1; k < 4; ++k) sacc += red[(k * 8 + w * 2 + c) * 64 + lane];
-          yv[c] = p3d_epi_apply(ep[c], sacc, wsq_any, p.bn, p.eps);
-          if (res) yv[c] += rv[c];
+          for (int k = 1; k < 4; ++k) sacc += red[((k * 4 + w) * NC + cc) * 64 + lane];
+          yv[cc] = p3d_epi_apply(ep[cc], sacc, wsq_any, p.bn, p.eps);
+          if (res) yv[cc] += rv[cc];
         }
         if (lastp) {
 #pragma unroll
-          for (int o = 0; o < NDT; ++o) {
-            f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int k = 0; k < UPM; ++k) {
+            if (!uv[k]) continue;
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
+            for (int o = 0; o < NDT; ++o) {
+              f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[c][e], wo[c][o][e], pacc, 0, 0, 0);
-            *(f32x4*)(pdst + (int64_t)u * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
+              for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[2 * k + c][e], wo[2 * k + c][o][e], pacc, 0, 0, 0);
+              *(f32x4*)(pdst + (int64_t)uu[k] * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
+            }
           }
         } else {
 #pragma unroll
-          for (int c = 0; c < 2; ++c) *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = yv[c];
+          for (int cc = 0; cc < NC; ++cc)
+            if (uv[cc >> 1])
+              *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * uu[cc >> 1] + (cc & 1)) * 64 + lane) * 4) = yv[cc];
         }
-        if (in_now) in_finish(u, nx, c0n);
-        // red / rsum are rewritten by this workgroup's next unit; after its last unit of the
-        // phase the group barrier's workgroup barrier orders the next phase's writes
-        if (u + n < U) __syncthreads();
+        if (lastp && has_next) {                 // the next step's input layer, these units
+#pragma unroll
+          for (int k = 0; k < UPM; ++k)
+            if (uv[k]) {
+              InOps nx;
+              in_load(uu[k], row0 + (int64_t)ng * 64, nx);
+              in_finish(uu[k], nx, c0n);
+            }
+        }
+        // red / rsum are rewritten by this workgroup's next contraction; after its last one
+        // of the phase the group barrier's workgroup barrier orders the next phase's writes
+        if (u + n * UPM < U) __syncthreads();
       }
       if (second) cur = t2;
       P3D_SERVE_STAMP(tr, 1);
