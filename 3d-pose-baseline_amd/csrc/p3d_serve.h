@@ -821,6 +821,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int k = 0; k < 16; ++k)
             if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
         }
+        const bool in_now = lastp && has_next;   // the next step's input layer, these units
         __builtin_amdgcn_sched_barrier(0);
         // ---- K-slice combine (LDS), epilogue ----------------------------------------------
 #pragma unroll
@@ -876,7 +877,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if (uv[cc >> 1])
               *(f32x4*)(Y + ((int64_t)(w * ngL + 2 * uu[cc >> 1] + (cc & 1)) * 64 + lane) * 4) = yv[cc];
         }
-        if (lastp && has_next) {                 // the next step's input layer, these units
+        // (requested here, not before the combine: held across it, the operands of both units
+        // pushed the kernel past 512 registers -- 200 spills, -18 %)
+        if (in_now) {
 #pragma unroll
           for (int k = 0; k < UPM; ++k)
             if (uv[k]) {
