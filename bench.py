@@ -257,9 +257,10 @@ def bench_serve(args, rank, world):
         for i in range(k):
             model.serve_device(xs[i % R], out=ys[i % R])
 
-    # untimed warmup: the W steps, and at least 3 launches (~20 ms) so the timed launches
-    # run at the clock the chip holds under this load (the first launches ran 5-12 % slower)
-    wl = max(3, -(-args.warmup // C))
+    # untimed warmup: the W steps, and at least 5 launches (~30 ms) so the timed launches
+    # run at the clock the chip holds under this load (the first launches ran 3-17 % slower:
+    # profiles/r01_v14_serve_launches.json)
+    wl = max(5, -(-args.warmup // C))
     run(wl)
     model.serve_check()
     barrier_sync(world)
