@@ -566,6 +566,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int NC = 2 * UPM;                // column tiles per contraction
   __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NC * 64]; // [slice][rt][ct][lane] (32 / 64 KB)
   __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64];        // split output reduction (4 KB)
+  // epilogue constants of this workgroup's first UPM units, per layer 0..2N and column tile:
+  // bias[16] | inv[16] = gamma / sqrt(var + eps) | shift[16] = beta - mean * inv, formed once
+  // per launch (the sqrt and divide of every epilogue element, and ~80 registers of BN operands
+  // held across the contraction, are gone)
+  __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * NC * 48];
   __shared__ int sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
@@ -636,6 +641,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // Write-after-read safety needs no more: a member writes its phase-p output only after its
   // K-combine barrier, i.e. after all four of its waves saw every member finish phase p-1, so
   // every read of the buffer being overwritten (last read in phase p-2 or earlier) is done.
+  {
+    const int nl = NH + 1;
+    for (int idx = tid; idx < nl * NC * 16; idx += 256) {
+      const int l = idx / (NC * 16), rem = idx % (NC * 16), cc = rem >> 4, j = rem & 15;
+      const int uk = r + (cc >> 1) * n;
+      float bb = 0.f, inv = 1.f, shift = 0.f;
+      if (uk < U) {
+        const ServeLayer& lyc = p.ly[l];
+        const int col = 16 * (2 * uk + (cc & 1)) + j;
+        bb = lyc.bias[col];
+        if (p.bn) {
+          inv = (1.0f / sqrtf(lyc.mvar[col] + p.eps)) * lyc.gamma[col];
+          shift = lyc.beta[col] - lyc.mmean[col] * inv;
+        }
+      }
+      float* e = ec + (l * NC + cc) * 48;
+      e[j] = bb; e[16 + j] = inv; e[32 + j] = shift;
+    }
+    __syncthreads();
+  }
+  // epilogue of column tile cc of layer l from the constants: z = acc / maxnorm + b,
+  // y = relu(z * inv + shift) -- the arithmetic of p3d_epi_apply
+  auto epi_c = [&](int l, int cc, f32x4 acc) -> f32x4 {
+    const float* e = ec + (l * NC + cc) * 48 + q4;
+    const f32x4 b4 = *(const f32x4*)e, inv4 = *(const f32x4*)(e + 16), sh4 = *(const f32x4*)(e + 32);
+    const float mx = wsq_any ? fmaxf(sqrtf(*p.ly[l].wsq), 1.0f) : 1.0f;
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float z = (wsq_any ? acc[k] / mx : acc[k]) + b4[k];
+      o[k] = fmaxf(p.bn ? z * inv4[k] + sh4[k] : z, 0.0f);
+    }
+    return o;
+  };
+
   auto group_sync = [&](bool full) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -661,7 +701,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // input layer of unit u for the step at row rbase into act buffer cbuf (row tile w, both
   // column tiles); operands as loaded by in_load
-  struct InOps { f32x4 xa[4], wb[2][4]; ServeEpi ep[2]; };
+  struct InOps { f32x4 xa[4], wb[2][4]; };
   auto in_load = [&](int u, int64_t rbase, InOps& o) {
     int64_t rowc = rbase + 16 * w + (lane & 15);
     rowc = rowc < p.M ? rowc : p.M - 1;
@@ -673,8 +713,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int c = 0; c < 2; ++c)
           o.wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
       }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) o.ep[c] = p3d_epi_load(li, 16 * (2 * u + c) + q4, p.bn, p.eps);
   };
   auto in_finish = [&](int u, const InOps& o, int cbuf) {
 #pragma unroll
@@ -685,8 +723,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (g < ngK0)
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o.wb[c][g][e], o.xa[g][e], acc, 0, 0, 0);
-      *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) =
-          p3d_epi_apply(o.ep[c], acc, wsq_any, p.bn, p.eps);
+      const int kk = (u - r) / n;               // which of this workgroup's units
+      f32x4 y;
+      if (kk < UPM) y = epi_c(0, 2 * kk + c, acc);
+      else y = p3d_epi_apply(p3d_epi_load(li, 16 * (2 * u + c) + q4, p.bn, p.eps), acc, wsq_any, p.bn, p.eps);
+      *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + 2 * u + c) * 64 + lane) * 4) = y;
     }
   };
 
@@ -762,13 +803,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int c = 0; c < 2; ++c) rb_[d][2 * k + c] = pre ? rbp[d][2 * k + c] : pbk[k][(c * ngL + d) * 64];
         }
         b_ready = false;
-        ServeEpi ep[NC];
         f32x4 rv[NC], wo[NC][NDT];
 #pragma unroll
         for (int cc = 0; cc < NC; ++cc) {
           const int col_t = 2 * uu[cc >> 1] + (cc & 1);
           const int64_t off = ((int64_t)(w * ngL + col_t) * 64 + lane) * 4;
-          ep[cc] = p3d_epi_load(ly, 16 * col_t + q4, p.bn, p.eps);
           rv[cc] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
           if (lastp) p3d_wo_load<NDT>(lo, col_t, ngL, wo[cc]);
         }
@@ -853,7 +892,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           f32x4 sacc = red[((0 * 4 + w) * NC + cc) * 64 + lane];   // slice 0, tile (w, cc)
 #pragma unroll
           for (int k = 1; k < 4; ++k) sacc += red[((k * 4 + w) * NC + cc) * 64 + lane];
-          yv[cc] = p3d_epi_apply(ep[cc], sacc, wsq_any, p.bn, p.eps);
+          if (first_u) yv[cc] = epi_c(ph, cc, sacc);
+          else yv[cc] = p3d_epi_apply(p3d_epi_load(ly, 16 * (2 * uu[cc >> 1] + (cc & 1)) + q4, p.bn, p.eps), sacc,
+                                      wsq_any, p.bn, p.eps);
           if (res) yv[cc] += rv[cc];
         }
         if (lastp) {
