@@ -1190,6 +1190,7 @@ struct p3d_model {
   int serve_grid = 0;
   int serve_groups = 0;     // at most this many groups take steps, 0 = all (env P3D_SERVE_GROUPS)
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
+  int serve_depth5 = 4;     // k_serve5 register-ring depth (env P3D_SERVE_DEPTH5, see serve5_depth)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1 or 2, with SPLIT >= 2)
@@ -1416,6 +1417,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_DEPTH5")) m->serve_depth5 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_KS")) m->serve_ks = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_W4")) m->serve_w4 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_SPLIT")) m->serve_split = atoi(ev);
@@ -1877,10 +1879,23 @@ static int serve_depth_for(const p3d_model* m, int L, int ks) {
   return d;
 }
 
+// k_serve5 ring depth actually launched: 4 / 2 / 1 for the paired SPLIT = 2 form, 2 / 1
+// otherwise (2 for paired SPLIT = 4); it must divide each wave's L / 64 k-groups.  Depth 8
+// spilled 186 registers and measured 8.1 M poses/s (vs 12.9 M at depth 4), so it is not built.
+static int serve5_depth(const p3d_model* m, int L) {
+  if (m->serve_split == 4 && m->serve_upm == 2) return 2;
+  const bool deep = m->serve_upm == 2 && m->serve_split == 2;
+  int d = m->serve_depth5;
+  if (d != 1 && d != 2 && d != 4) d = 4;
+  if (!deep && d > 2) d = 2;
+  while (d > 1 && (L / 64) % d != 0) d >>= 1;
+  return d;
+}
+
 template <int NDT>
 static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned grid, hipStream_t st, const ServeArgs& a) {
   if (m->serve_w4 == 5 && a.nblk > 0) {   // k_serve5: 4-wave workgroups, steps software-pipelined
-    const int d = serve_depth_for(m, a.L, 4);
+    const int d = serve5_depth(m, a.L);
     // paired units (UPM = 2, env P3D_SERVE_UPM) where a group has about U/2 members
     const bool pair = m->serve_upm == 2 && m->serve_split >= 2;
     if (m->serve_split == 4) {
@@ -1888,7 +1903,8 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
       else if (d == 2) go(ps, k_serve5<2, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
       else go(ps, k_serve5<1, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
     } else if (m->serve_split == 2) {
-      if (pair && d == 2) go(ps, k_serve5<2, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
+      if (pair && d == 4) go(ps, k_serve5<4, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
+      else if (pair && d == 2) go(ps, k_serve5<2, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
       else if (pair) go(ps, k_serve5<1, NDT, 2, 2>, dim3(grid), dim3(256), st, a);
       else if (d == 2) go(ps, k_serve5<2, NDT, 2, 1>, dim3(grid), dim3(256), st, a);
       else go(ps, k_serve5<1, NDT, 2, 1>, dim3(grid), dim3(256), st, a);
@@ -2333,7 +2349,7 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     {
       const int sp = m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1;
       const int upm = (m->serve_upm == 2 && sp >= 2) ? 2 : 1;
-      const int d = (upm == 2 && sp == 4) ? 2 : serve_depth_for(m, m->cfg.linear_size, 4);
+      const int d = serve5_depth(m, m->cfg.linear_size);
       n = "k_serve5<" + std::to_string(d) + ", " + std::to_string(ndt) + ", " + std::to_string(sp) + ", " +
           std::to_string(upm) + ">";
     }

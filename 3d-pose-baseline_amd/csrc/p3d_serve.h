@@ -50,6 +50,9 @@
 #ifndef P3D_SERVE_EPI_EARLY        // bias / BN / residual / W4 operands requested before the contraction
 #define P3D_SERVE_EPI_EARLY 1
 #endif
+#ifndef P3D_SERVE_RV_LATE          // k_serve5: residual operands requested after the contraction
+#define P3D_SERVE_RV_LATE 1
+#endif
 
 // Phase timestamps for development (-DP3D_TRACE, tools/trace_serve.py): workgroup rank 0
 // (and rank 1) of every XCD group, first 8 local steps, up to 8 stamps per phase (0 begin,
@@ -731,7 +734,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  f32x4 rbp[DEPTH][NC];                      // the next ring's first weight fragments
+  constexpr int PD = DEPTH < 2 ? DEPTH : 2;  // ring slots prefetched off-contraction
+  f32x4 rbp[PD][NC];                         // the next ring's first weight fragments
   bool b_ready = false;
   auto b_prefetch = [&](int layer, int unit) {   // units unit, unit + n (UPM = 2)
     if (unit >= U) return;
@@ -740,7 +744,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int uk = (unit + k * n < U) ? unit + k * n : unit;
       const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)(2 * uk) * ngL + gb) * 64 + lane;
 #pragma unroll
-      for (int d = 0; d < DEPTH; ++d)
+      for (int d = 0; d < PD; ++d)
 #pragma unroll
         for (int c = 0; c < 2; ++c) rbp[d][2 * k + c] = pbn[(c * ngL + d) * 64];
     }
@@ -800,17 +804,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int k = 0; k < UPM; ++k)
 #pragma unroll
-            for (int c = 0; c < 2; ++c) rb_[d][2 * k + c] = pre ? rbp[d][2 * k + c] : pbk[k][(c * ngL + d) * 64];
+            for (int c = 0; c < 2; ++c)
+              rb_[d][2 * k + c] = (pre && d < PD) ? rbp[d < PD ? d : 0][2 * k + c] : pbk[k][(c * ngL + d) * 64];
         }
         b_ready = false;
         f32x4 rv[NC], wo[NC][NDT];
+        auto rv_load = [&]() {                   // residual operands of the epilogue
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-          const int col_t = 2 * uu[cc >> 1] + (cc & 1);
-          const int64_t off = ((int64_t)(w * ngL + col_t) * 64 + lane) * 4;
-          rv[cc] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
-          if (lastp) p3d_wo_load<NDT>(lo, col_t, ngL, wo[cc]);
-        }
+          for (int cc = 0; cc < NC; ++cc) {
+            const int col_t = 2 * uu[cc >> 1] + (cc & 1);
+            const int64_t off = ((int64_t)(w * ngL + col_t) * 64 + lane) * 4;
+            rv[cc] = res ? p3d_ld_sc1(p3d_rsrc(res), (int)(off * 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        };
+        if (!P3D_SERVE_RV_LATE) rv_load();
         f32x4 acc[NC][4];
 #pragma unroll
         for (int cc = 0; cc < NC; ++cc)
@@ -859,6 +866,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int k = 0; k < 16; ++k)
             if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
+        }
+        if (P3D_SERVE_RV_LATE) rv_load();
+        if (lastp) {                             // output-layer operands of the fused partial
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) p3d_wo_load<NDT>(lo, 2 * uu[cc >> 1] + (cc & 1), ngL, wo[cc]);
         }
         const bool in_now = lastp && has_next;   // the next step's input layer, these units
         __builtin_amdgcn_sched_barrier(0);
