@@ -11,6 +11,7 @@ import csv
 import glob
 import json
 import os
+import sqlite3
 import sys
 
 
@@ -21,6 +22,11 @@ def load(d, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") == counter:
                 acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    for db in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):   # rocpd format
+        q = ("select kernel_name, dispatch_id, sum(value) from counters_collection "
+             "where counter_name = ? group by dispatch_id order by dispatch_id")
+        for name, _, v in sqlite3.connect(db).execute(q, (counter,)):
+            acc[name].append(float(v))
     return acc
 
 
