@@ -1193,7 +1193,7 @@ struct p3d_model {
   int serve_depth5 = 4;     // k_serve5 register-ring depth (env P3D_SERVE_DEPTH5, see serve5_depth)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
-  int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1 or 2, with SPLIT >= 2)
+  int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -1883,7 +1883,7 @@ static int serve_depth_for(const p3d_model* m, int L, int ks) {
 // otherwise (2 for paired SPLIT = 4); it must divide each wave's L / 64 k-groups.  Depth 8
 // spilled 186 registers and measured 8.1 M poses/s (vs 12.9 M at depth 4), so it is not built.
 static int serve5_depth(const p3d_model* m, int L) {
-  if (m->serve_split == 4 && m->serve_upm == 2) return 2;
+  if (m->serve_split == 4 && m->serve_upm >= 2) return 2;
   const bool deep = m->serve_upm == 2 && m->serve_split == 2;
   int d = m->serve_depth5;
   if (d != 1 && d != 2 && d != 4) d = 4;
@@ -1899,7 +1899,9 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
     // paired units (UPM = 2, env P3D_SERVE_UPM) where a group has about U/2 members
     const bool pair = m->serve_upm == 2 && m->serve_split >= 2;
     if (m->serve_split == 4) {
-      if (pair) go(ps, k_serve5<2, NDT, 4, 2>, dim3(grid), dim3(256), st, a);
+      if (m->serve_upm == 4 && 2 * a.nblk + 1 <= P3D_SERVE_ECL(8))
+        go(ps, k_serve5<2, NDT, 4, 4>, dim3(grid), dim3(256), st, a);
+      else if (pair) go(ps, k_serve5<2, NDT, 4, 2>, dim3(grid), dim3(256), st, a);
       else if (d == 2) go(ps, k_serve5<2, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
       else go(ps, k_serve5<1, NDT, 4, 1>, dim3(grid), dim3(256), st, a);
     } else if (m->serve_split == 2) {
@@ -2348,7 +2350,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     if (m->serve_w4 == 5 && m->cfg.num_layers > 0)
     {
       const int sp = m->serve_split == 4 ? 4 : m->serve_split == 2 ? 2 : 1;
-      const int upm = (m->serve_upm == 2 && sp >= 2) ? 2 : 1;
+      const int upm = (m->serve_upm == 4 && sp == 4 && 2 * m->cfg.num_layers + 1 <= P3D_SERVE_ECL(8)) ? 4
+                      : (m->serve_upm == 2 && sp >= 2) ? 2 : 1;
       const int d = serve5_depth(m, m->cfg.linear_size);
       n = "k_serve5<" + std::to_string(d) + ", " + std::to_string(ndt) + ", " + std::to_string(sp) + ", " +
           std::to_string(upm) + ">";

@@ -38,6 +38,18 @@
 #include "p3d_kernels.h"
 
 #define P3D_SERVE_MAXL 16          // input + 2*blocks + output layers
+// layers whose epilogue constants k_serve5 keeps in LDS (input + hidden): 15, or 9 (N <= 4
+// blocks) for the 8-column-tile form, whose K-combine buffer takes 128 KB
+#ifndef P3D_S4_RE                  // 8-column-tile form (SPLIT 4, UPM 4) variants
+#define P3D_S4_RE 2                // output-reduction elements per lane
+#endif
+#ifndef P3D_S4_WOPIPE
+#define P3D_S4_WOPIPE 0            // next unit's output-layer operands during this unit's partial
+#endif
+#ifndef P3D_S4_INPIPE
+#define P3D_S4_INPIPE 0            // next unit's input-layer operands during this unit's layer
+#endif
+#define P3D_SERVE_ECL(NC) ((NC) >= 8 ? 9 : P3D_SERVE_MAXL - 1)
 #define P3D_SERVE_SYNC_WORDS 2112  // [0..7] census, [8] arrivals, [64 + 64*g + r] flag of member r of group g
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
@@ -568,12 +580,14 @@ template <int DEPTH, int NDT, int SPLIT, int UPM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve5(ServeArgs p) {
   constexpr int NC = 2 * UPM;                // column tiles per contraction
   __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NC * 64]; // [slice][rt][ct][lane] (32 / 64 KB)
-  __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64];        // split output reduction (4 KB)
+  // split output reduction: RE elements per lane (a group of 8 members has 96 per workgroup)
+  constexpr int RE = UPM >= 4 ? P3D_S4_RE : 1;
+  __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64 * RE];   // (4 / 8 KB)
   // epilogue constants of this workgroup's first UPM units, per layer 0..2N and column tile:
   // bias[16] | inv[16] = gamma / sqrt(var + eps) | shift[16] = beta - mean * inv, formed once
   // per launch (the sqrt and divide of every epilogue element, and ~80 registers of BN operands
   // held across the contraction, are gone)
-  __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * NC * 48];
+  __shared__ __attribute__((aligned(16))) float ec[P3D_SERVE_ECL(NC) * NC * 48];
   __shared__ int sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
@@ -634,7 +648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int gb = (ngL * w) >> 2, gcount = ngL >> 2;   // this wave's K slice
   // this workgroup's share of a step's output elements, split over (slice, element) threads
   const int es = (int)(((int64_t)E4 * r) / n), ecnt = (int)(((int64_t)E4 * (r + 1)) / n) - es;
-  const bool split_red = r < U && ecnt <= 64 && U <= 64;
+  const bool split_red = r < U && ecnt <= 64 * RE && U <= 64 / RE;
   const int rsl = w, rei = lane;             // slice = this wave's producers' units
 
   // Group barrier: drain, one lane publishes this member's phase, then every wave waits only
@@ -705,17 +719,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // input layer of unit u for the step at row rbase into act buffer cbuf (row tile w, both
   // column tiles); operands as loaded by in_load
   struct InOps { f32x4 xa[4], wb[2][4]; };
+  auto in_load_w = [&](int u, InOps& o) {     // the unit's input-layer weight fragments
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g < ngK0)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          o.wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
+  };
   auto in_load = [&](int u, int64_t rbase, InOps& o) {
     int64_t rowc = rbase + 16 * w + (lane & 15);
     rowc = rowc < p.M ? rowc : p.M - 1;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
-      if (g < ngK0) {
-        o.xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-          o.wb[c][g] = *(const f32x4*)(li.Wf + ((int64_t)((2 * u + c) * ngK0 + g) * 64 + lane) * 4);
-      }
+      if (g < ngK0) o.xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+    in_load_w(u, o);
   };
   auto in_finish = [&](int u, const InOps& o, int cbuf) {
 #pragma unroll
@@ -734,7 +752,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  constexpr int PD = DEPTH < 2 ? DEPTH : 2;  // ring slots prefetched off-contraction
+  // ring slots prefetched off-contraction (one for the 8-column-tile form: register budget)
+  constexpr int PD = UPM >= 4 ? 1 : DEPTH < 2 ? DEPTH : 2;
+  // output-layer operands of the fused partial: all units' before the combine, or (8 column
+  // tiles, register budget) the first unit's before it and each next unit's while the
+  // current one's partial is formed (two units' worth of registers)
+  constexpr bool WO_LATE = UPM >= 4;
+  constexpr int NWO = WO_LATE ? 2 + 2 * P3D_S4_WOPIPE : NC;
   f32x4 rbp[PD][NC];                         // the next ring's first weight fragments
   bool b_ready = false;
   auto b_prefetch = [&](int layer, int unit) {   // units unit, unit + n (UPM = 2)
@@ -808,7 +832,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
               rb_[d][2 * k + c] = (pre && d < PD) ? rbp[d < PD ? d : 0][2 * k + c] : pbk[k][(c * ngL + d) * 64];
         }
         b_ready = false;
-        f32x4 rv[NC], wo[NC][NDT];
+        f32x4 rv[NC], wo[NWO][NDT];
         auto rv_load = [&]() {                   // residual operands of the epilogue
 #pragma unroll
           for (int cc = 0; cc < NC; ++cc) {
@@ -858,19 +882,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (u + n * UPM < U) b_prefetch(ph, u + n * UPM);   // this workgroup's next unit(s)
         else if (!lastp) b_prefetch(ph + 1, r);              // the next layer's first unit(s)
         else if (has_next) b_prefetch(1, r);                 // the next step's first layer
-        f32x4 rpv[16];
+        constexpr int KR = 16 / RE;              // units per slice (U <= 64 / RE)
+        f32x4 rpv[RE][KR];
         const bool red_now = red_here && split_red && first_u && rei < ecnt;
         if (red_now) {
           const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(prev_part);
           const int ub = (U * rsl) >> 2, ue = (U * (rsl + 1)) >> 2;
 #pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (ub + k < ue) rpv[k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei) * 16);
+          for (int j = 0; j < RE; ++j)
+#pragma unroll
+            for (int k = 0; k < KR; ++k)
+              if (ub + k < ue && rei + 64 * j < ecnt)
+                rpv[j][k] = p3d_ld_sc1(rp, ((ub + k) * E4 + es + rei + 64 * j) * 16);
         }
         if (P3D_SERVE_RV_LATE) rv_load();
         if (lastp) {                             // output-layer operands of the fused partial
 #pragma unroll
-          for (int cc = 0; cc < NC; ++cc) p3d_wo_load<NDT>(lo, 2 * uu[cc >> 1] + (cc & 1), ngL, wo[cc]);
+          for (int cc = 0; cc < (WO_LATE ? 2 * P3D_S4_WOPIPE : NC); ++cc)
+            p3d_wo_load<NDT>(lo, 2 * uu[cc >> 1] + (cc & 1), ngL, wo[cc]);
         }
         const bool in_now = lastp && has_next;   // the next step's input layer, these units
         __builtin_amdgcn_sched_barrier(0);
@@ -880,22 +909,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int t = 0; t < 4; ++t) red[((w * 4 + t) * NC + cc) * 64 + lane] = acc[cc][t];
         if (red_here && split_red && first_u) {
-          f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (red_now) {
-            const int ub = (U * rsl) >> 2, ue = (U * (rsl + 1)) >> 2;
-            if (ub < ue) ss = rpv[0];
 #pragma unroll
-            for (int k = 1; k < 16; ++k)
-              if (ub + k < ue) ss += rpv[k];
+          for (int j = 0; j < RE; ++j) {
+            f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (red_now && rei + 64 * j < ecnt) {
+              const int ub = (U * rsl) >> 2, ue = (U * (rsl + 1)) >> 2;
+              if (ub < ue) ss = rpv[j][0];
+#pragma unroll
+              for (int k = 1; k < KR; ++k)
+                if (ub + k < ue) ss += rpv[j][k];
+            }
+            rsum[rsl * 64 * RE + rei + 64 * j] = ss;
           }
-          rsum[rsl * 64 + rei] = ss;
         }
         __syncthreads();
         P3D_SERVE_STAMP(tr, 4);
         if (red_here && split_red && first_u && tid < ecnt) {
           f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 + tid];
+          for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 * RE + tid];
           p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
         }
         f32x4 yv[NC];
@@ -913,6 +945,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int k = 0; k < UPM; ++k) {
             if (!uv[k]) continue;
+            if (WO_LATE && P3D_S4_WOPIPE && k + 1 < UPM && uv[k + 1]) {
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+                p3d_wo_load<NDT>(lo, 2 * uu[k + 1] + c, ngL, wo[P3D_S4_WOPIPE ? 2 * ((k + 1) & 1) + c : c]);
+            } else if (WO_LATE && !P3D_S4_WOPIPE) {
+#pragma unroll
+              for (int c = 0; c < 2; ++c) p3d_wo_load<NDT>(lo, 2 * uu[k] + c, ngL, wo[c]);
+            }
 #pragma unroll
             for (int o = 0; o < NDT; ++o) {
               f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -920,7 +960,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
               for (int c = 0; c < 2; ++c)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                  pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[2 * k + c][e], wo[2 * k + c][o][e], pacc, 0, 0, 0);
+                  pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[2 * k + c][e], wo[WO_LATE ? (P3D_S4_WOPIPE ? 2 * (k & 1) + c : c) : 2 * k + c][o][e], pacc,
+                                                              0, 0, 0);
               *(f32x4*)(pdst + (int64_t)uu[k] * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
             }
           }
@@ -932,12 +973,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         // (requested here, not before the combine: held across it, the operands of both units
         // pushed the kernel past 512 registers -- 200 spills, -18 %)
-        if (in_now) {
+        // the step's input rows are loaded once for all of this contraction's units; one
+        // unit's weights at a time (all of them hoisted together spill)
+        if (in_now && UPM >= 4 && P3D_S4_INPIPE) {               // one unit's operands in flight ahead
+          InOps nx[2];
+          in_load(uu[0], row0 + (int64_t)ng * 64, nx[0]);
 #pragma unroll
-          for (int k = 0; k < UPM; ++k)
+          for (int k = 0; k < UPM; ++k) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (k + 1 < UPM && uv[k + 1]) in_load(uu[k + 1], row0 + (int64_t)ng * 64, nx[(k + 1) & 1]);
+            if (uv[k]) in_finish(uu[k], nx[k & 1], c0n);
+          }
+        } else if (in_now) {
+          InOps nx;
+          in_load(uu[0], row0 + (int64_t)ng * 64, nx);
+          in_finish(uu[0], nx, c0n);
+#pragma unroll
+          for (int k = 1; k < UPM; ++k)
             if (uv[k]) {
-              InOps nx;
-              in_load(uu[k], row0 + (int64_t)ng * 64, nx);
+              __builtin_amdgcn_sched_barrier(0);
+              in_load_w(uu[k], nx);
               in_finish(uu[k], nx, c0n);
             }
         }

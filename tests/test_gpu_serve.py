@@ -117,3 +117,26 @@ def test_serve_rejects_bad_shapes():
     with pytest.raises(ValueError):
         m.serve_device(torch.zeros((64, 31), device="cuda"))
     m.close()
+
+
+@pytest.mark.parametrize("split,upm,depth", [(2, 2, 4), (2, 2, 2), (2, 1, 2), (1, 1, 2), (4, 2, 2), (4, 4, 2)])
+@pytest.mark.parametrize("L,N", [(1024, 2), (256, 1), (2048, 1)])
+def test_serve_knob_variants_vs_oracle(monkeypatch, split, upm, depth, L, N):
+    """Every k_serve5 form the P3D_SERVE_SPLIT / _UPM / _DEPTH5 knobs select (read at
+    p3d_create) gives the oracle's outputs, including groups with fewer members than units
+    per contraction (L = 256) and several contractions per phase (L = 2048)."""
+    monkeypatch.setenv("P3D_SERVE_SPLIT", str(split))
+    monkeypatch.setenv("P3D_SERVE_UPM", str(upm))
+    monkeypatch.setenv("P3D_SERVE_DEPTH5", str(depth))
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    B = 64 * 300 + 13
+    x = np.random.default_rng(L + split * 10 + upm).standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    y = m.serve_device(xd)
+    torch.cuda.synchronize()
+    m.serve_check()
+    idx = np.r_[0:64, np.random.default_rng(1).choice(B, 448, replace=False), B - 13:B]
+    ro, _ = ref_mlp.forward(st, x[idx], False, 1.0, 0, 0, 0)
+    close(y.cpu().numpy()[idx], ro)
+    m.close()
