@@ -1193,6 +1193,7 @@ struct p3d_model {
   int serve_depth5 = 4;     // k_serve5 register-ring depth (env P3D_SERVE_DEPTH5, see serve5_depth)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
+  std::vector<hipEvent_t> gev;   // per-layer gradient-ready events (p3d_grad_events)
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
@@ -1466,6 +1467,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
 
 extern "C" int p3d_destroy(p3d_model* m) {
   if (!m) return P3D_OK;
+  for (hipEvent_t e : m->gev) (void)hipEventDestroy(e);
   free_all(m);
   delete m;
   return P3D_OK;
@@ -2107,6 +2109,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         int rc = launch_wgrad(m, wa, st);
         if (rc) return rc;
       }
+      if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[0], st));
       break;
     }
     const Layer& pv = m->layers[l - 1];
@@ -2176,6 +2179,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       int rc = launch_wgrad(m, wa, st);
       if (rc) return rc;
     }
+    // layer l's W and b (wgrad above) and its gamma/beta (bn_bwd of iteration l + 1) are final
+    if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[l], st));
     dz_cur = m->dz[l - 1];
     dz_pk = true;
   }
@@ -2187,7 +2192,36 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     LAUNCH_CHECK("k_dot_final");
     k_maxnorm_grad<<<dim3(64, m->wtab.n), 256, 0, st>>>(grads, params, m->wtab, m->wsq, m->gw);
     LAUNCH_CHECK("k_maxnorm_grad");
+    for (hipEvent_t e : m->gev) HIP_TRY(hipEventRecord(e, st));
   }
+  return P3D_OK;
+}
+
+extern "C" int p3d_grad_events(p3d_model* m, int32_t enable) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_grad_events: null model");
+  for (hipEvent_t e : m->gev) HIP_TRY(hipEventDestroy(e));
+  m->gev.clear();
+  if (enable) {
+    m->gev.resize(m->layers.size(), nullptr);
+    for (hipEvent_t& e : m->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  return P3D_OK;
+}
+
+// flat range of layer l's trainables (TF creation order: W, b[, gamma, beta]), padding included
+extern "C" int p3d_layer_grad_range(const p3d_model* m, int32_t layer, int64_t* begin, int64_t* end) {
+  if (!m || !begin || !end) return fail(P3D_ERR_ARG, "p3d_layer_grad_range: null argument");
+  if (layer < 0 || layer >= (int32_t)m->layers.size()) return fail(P3D_ERR_ARG, "p3d_layer_grad_range: bad layer");
+  *begin = m->layers[layer].w;
+  *end = layer + 1 < (int32_t)m->layers.size() ? m->layers[layer + 1].w : m->n_flat;
+  return P3D_OK;
+}
+
+extern "C" int p3d_stream_wait_grad(p3d_model* m, int32_t layer, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_stream_wait_grad: null model");
+  if (m->gev.empty()) return fail(P3D_ERR_STATE, "p3d_stream_wait_grad: p3d_grad_events not enabled");
+  if (layer < 0 || layer >= (int32_t)m->gev.size()) return fail(P3D_ERR_ARG, "p3d_stream_wait_grad: bad layer");
+  HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, m->gev[layer], 0));
   return P3D_OK;
 }
 

@@ -52,6 +52,52 @@ def allreduce_mean_(t):
     return t
 
 
+def plan_buckets(ranges, min_elems):
+    """Group per-layer gradient ranges into all-reduce buckets, in backward order.
+
+    ``ranges[l] = (begin, end)`` is layer l's slice of the flat gradient buffer (layers
+    are contiguous in TF creation order, layer 0 first).  The backward finishes the
+    output layer first, so buckets are formed from the last layer down; a bucket closes
+    once it holds ``min_elems`` floats and is ready when its lowest layer is.  A short
+    remainder joins the previous bucket.  Returns [(begin, end, ready_layer)], covering
+    every range exactly once.
+    """
+    out = []
+    hi = None
+    for l in range(len(ranges) - 1, -1, -1):
+        lo, e = ranges[l]
+        if hi is None:
+            hi = e
+        if hi - lo >= min_elems or l == 0:
+            out.append([lo, hi, l])
+            hi = None
+    if len(out) > 1 and out[-1][1] - out[-1][0] < min_elems:
+        lo, _, l = out.pop()
+        out[-1][0], out[-1][2] = lo, l
+    return [tuple(b) for b in out]
+
+
+def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
+    """Bucketed DP gradient average that overlaps the backward (RCCL only).
+
+    For each bucket (backward order), ``comm_stream`` waits for its layer's
+    gradient-ready event (``wait_ready(layer, stream_handle)``, p3d_stream_wait_grad),
+    then an async all-reduce(AVG) of that slice is issued from it; the current stream
+    finally waits for all of them.  Every byte of ``t`` is reduced exactly once, so the
+    result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).
+    """
+    import torch
+    import torch.distributed as dist
+    works = []
+    with torch.cuda.stream(comm_stream):
+        for lo, hi, layer in buckets:
+            wait_ready(layer, comm_stream.cuda_stream)
+            works.append(dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG, async_op=True))
+    for w in works:
+        w.wait()
+    return t
+
+
 def allreduce_sum_(t):
     import torch.distributed as dist
     on, _, world = dist_state()

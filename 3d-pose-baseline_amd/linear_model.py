@@ -462,7 +462,10 @@ class LinearModel(object):
                                        self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
                   "p3d_train_step")
         else:
-            # forward + fused MSE + backward, all-reduce of the flat gradient, TF1 Adam
+            # forward + fused MSE + backward, all-reduce of the flat gradient (in buckets that
+            # overlap the backward under RCCL), TF1 Adam
+            if getattr(self, "_buckets", False) is False:   # first DP step: the default plan,
+                self.dp_buckets()                            # events on before the backward
             check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
                                           self.rank * B, ptr(loss_t), self.stream()), "p3d_train_fwd_bwd")
             self._allreduce_grads()
@@ -484,8 +487,35 @@ class LinearModel(object):
         check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
         return loss, y
 
+    def dp_buckets(self, bucket_mb=None):
+        """Enable (bucket_mb > 0) or disable (0) the bucketed gradient all-reduce that
+        overlaps the backward (RCCL only; env P3D_DP_BUCKET_MB, default 4 MB).  Must be
+        called before a backward is issued.  Returns the bucket plan [(begin, end, layer)]."""
+        import ctypes
+        import torch.distributed as dist
+        if bucket_mb is None:
+            bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "4"))
+        on = (bucket_mb > 0 and self.data_parallel and dist.is_initialized()
+              and dist.get_backend() == "nccl")
+        check(lib().p3d_grad_events(self._h, 1 if on else 0), "p3d_grad_events")
+        self._buckets = None
+        if on:
+            ranges = []
+            for l in range(2 * self.num_layers + 2):
+                b, e = ctypes.c_int64(), ctypes.c_int64()
+                check(lib().p3d_layer_grad_range(self._h, l, ctypes.byref(b), ctypes.byref(e)), "p3d_layer_grad_range")
+                ranges.append((b.value, e.value))
+            self._buckets = dist_utils.plan_buckets(ranges, int(bucket_mb * (1 << 20)) // 4)
+            self._comm = self.torch.cuda.Stream(device=self.device)
+        return self._buckets
+
     def _allreduce_grads(self):
-        dist_utils.allreduce_mean_(self.flat["grads"])
+        if getattr(self, "_buckets", None):
+            def wait(layer, handle):
+                check(lib().p3d_stream_wait_grad(self._h, layer, handle), "p3d_stream_wait_grad")
+            dist_utils.allreduce_mean_buckets_(self.flat["grads"], self._buckets, wait, self._comm)
+        else:
+            dist_utils.allreduce_mean_(self.flat["grads"])
 
     # ------------------------------------------------------------------ reference API
     def step(self, session, encoder_inputs, decoder_outputs, dropout_keep_prob, isTraining=True):

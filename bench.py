@@ -391,15 +391,18 @@ def bench_infer(args, rank, world):
     return value, dt, roof, single
 
 
-def bench_train(args, rank, world, steps=None, warmup=None):
+def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
     """cfg3: K training steps (fwd + MSE + bwd + [all-reduce] + fused TF1 Adam/re-pack) of
     64 poses per GPU.  Single GPU: G steps captured in one HIP graph (all step state is
     device-resident: dropout counter, lr decay, beta powers).  Data parallel: eager steps
-    with one RCCL all-reduce(AVG) of the 17.17 MB flat gradient per step."""
+    with RCCL all-reduce(AVG) of the 17.17 MB flat gradient per step, in buckets of
+    ``bucket_mb`` that overlap the backward (0: one all-reduce after it)."""
     import torch
     steps = steps or args.steps
     warmup = warmup if warmup is not None else args.warmup
     model, _ = make_model(data_parallel=world > 1)
+    if world > 1:
+        model.dp_buckets(args.dp_bucket_mb if bucket_mb is None else bucket_mb)
     rng = np.random.default_rng(200 + rank)
     G = 16
     while steps % G:
@@ -813,6 +816,8 @@ def main():
     ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
     ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
     ap.add_argument("--keep", type=float, default=0.5, help="dropout keep_prob of the train step")
+    ap.add_argument("--dp-bucket-mb", type=float, default=4.0,
+                    help="data-parallel gradient all-reduce bucket (MB) overlapping the backward; 0 = one all-reduce")
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
@@ -852,6 +857,14 @@ def main():
                          "roofline": troof}
             except Exception as exc:  # report, never lose the headline line
                 train = {"error": repr(exc)[:300]}
+            if world > 1 and args.dp_bucket_mb > 0 and "error" not in train:
+                try:   # the same steps with one all-reduce after the backward (no overlap)
+                    sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=0)
+                    train["dp_bucket_mb"] = args.dp_bucket_mb
+                    train["single_allreduce"] = {"value": round(sv, 1), "unit": "poses/s",
+                                                 "ms_per_step": round(1000.0 * sdt / args.train_steps, 5)}
+                except Exception as exc:
+                    train["single_allreduce"] = {"error": repr(exc)[:300]}
         if not args.no_eval:
             try:
                 sweep = bench_eval(args, rank, world)

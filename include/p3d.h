@@ -137,6 +137,18 @@ int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, f
                       float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,
                       void* stream);
 
+/* Gradient-ready events for a bucketed data-parallel all-reduce (the DP form of
+ * opt.compute_gradients -> apply_gradients, linear_model.py:143-145).
+ * p3d_grad_events(m, 1) makes every later p3d_backward / p3d_train_fwd_bwd record one event
+ * per layer l (0 = input layer .. 2N+1 = output layer) on its stream as soon as the flat grads
+ * range [begin, end) of p3d_layer_grad_range(m, l) is final -- the output layer's first, the
+ * input layer's last, so the all-reduce of late layers overlaps the backward of earlier ones.
+ * p3d_stream_wait_grad makes another stream wait for layer l's event of the last backward.
+ * (--max_norm models: every event after the clip's gradient, i.e. at the end.) */
+int p3d_grad_events(p3d_model* m, int32_t enable);
+int p3d_layer_grad_range(const p3d_model* m, int32_t layer, int64_t* begin, int64_t* end);
+int p3d_stream_wait_grad(p3d_model* m, int32_t layer, void* stream);
+
 /* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
  * the TF1 Adam update, global_step += 1.  With env P3D_FUSE_ADAM=1 at p3d_create the update
  * runs inside the weight-gradient kernels instead (no separate optimizer pass; the flat

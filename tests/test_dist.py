@@ -137,3 +137,24 @@ def test_shard_range_partition():
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in parts) - min(h - l for l, h in parts) <= 1
+
+
+def test_plan_buckets_cover_backward_order():
+    """DP gradient buckets (dist_utils.plan_buckets): every layer range exactly once,
+    formed from the output layer down, each ready with its lowest layer."""
+    import dist_utils
+    # cfg2-like flat layout: input 32x1024 (+b, gamma, beta), 4 hidden 1024^2 (+3x1024), output 1024x48 (+48)
+    sizes = [32 * 1024 + 3 * 1024] + [1024 * 1024 + 3 * 1024] * 4 + [1024 * 48 + 64]
+    ranges, off = [], 0
+    for s in sizes:
+        ranges.append((off, off + s))
+        off += s
+    plan = dist_utils.plan_buckets(ranges, (4 << 20) // 4)
+    assert [b[2] for b in plan] == sorted((b[2] for b in plan), reverse=True)
+    cov = sorted((lo, hi) for lo, hi, _ in plan)
+    assert cov[0][0] == 0 and cov[-1][1] == off and all(a[1] == b[0] for a, b in zip(cov, cov[1:]))
+    for lo, hi, layer in plan:       # ready layer = the lowest layer the bucket touches
+        assert ranges[layer][0] == lo
+    assert len(plan) == 4 and plan[-1][2] == 0      # the short input-layer remainder joined
+    assert dist_utils.plan_buckets(ranges, 1) == [(r[0], r[1], l) for l, r in reversed(list(enumerate(ranges)))]
+    assert dist_utils.plan_buckets(ranges, off * 2) == [(0, off, 0)]
