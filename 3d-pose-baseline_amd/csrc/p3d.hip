@@ -787,17 +787,18 @@ __device__ __forceinline__ void p3d_stage64(float* __restrict__ dst, const float
   }
 }
 
-__global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
+// dW tile (bx, by) = 64 columns x 64 rows of X^T dZ (and db from the by == 0 row of tiles)
+__device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
   __shared__ __attribute__((aligned(16))) float xs[64 * WG_LDS_STRIDE];
   __shared__ __attribute__((aligned(16))) float zs[64 * WG_LDS_STRIDE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int n0 = bx * 64, k0 = by * 64;
   f32x4 acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   __shared__ float dbp[4][64];
-  const bool do_db = p.db && blockIdx.y == 0;
+  const bool do_db = p.db && by == 0;
   float dbs = 0.f;   // wave w: rows 16w .. 16w+15 of column `lane` (summed in row order)
   for (int mc = 0; mc < p.M; mc += 64) {
     p3d_stage64(xs, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
@@ -838,7 +839,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
       }
     }
   }
-  if (p.adam && p.bn_adam && blockIdx.x == 0 && tid < 64 && k0 + tid < p.K) {
+  if (p.adam && p.bn_adam && bx == 0 && tid < 64 && k0 + tid < p.K) {
     const float omb1 = 1.0f - p.af.b1, omb2 = 1.0f - p.af.b2;
     const int64_t og = p.goff + k0 + tid, ob = p.btoff + k0 + tid;
     float w1 = p.w[og], m1 = p.m[og], v1 = p.v[og];
@@ -868,6 +869,36 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) {
       const int n = n0 + 16 * s + i;
       if (k < p.K && n < p.N) p.dW[(int64_t)k * p.N + n] = acc[s][r];
     }
+}
+
+__global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) { p3d_wgrad_tile(p, blockIdx.x, blockIdx.y); }
+
+// Every layer's weight gradient in ONE launch (backward without fused Adam or gradient-ready
+// events): a layer's dW / db depend only on its dZ and its input activations, which nothing
+// later in the backward overwrites, so they can all wait for its end.  One grid over the
+// tiles of all layers (1,056 workgroups at cfg2) replaces 2N + 2 launches of <= 256
+// workgroups; every tile's arithmetic is k_wgrad's, so the gradients are bit-identical.
+#define P3D_WG_MULTI 16
+struct WgradLayer {
+  const float* X; const float* dZ; float* dW; float* db;
+  int64_t ldx, ldz; int xpk, zpk, M, K, N;
+};
+struct WgradMulti {
+  int n;
+  int begin[P3D_WG_MULTI + 1];   // workgroup prefix over layers
+  int gx[P3D_WG_MULTI];          // column tiles of each layer
+  WgradLayer ly[P3D_WG_MULTI];
+};
+__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < mw.n && b >= mw.begin[j + 1]) ++j;
+  const WgradLayer& l = mw.ly[j];
+  WgradArgs p{};
+  p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
+  p.M = l.M; p.K = l.K; p.N = l.N; p.dW = l.dW; p.db = l.db;
+  const int loc = b - mw.begin[j];
+  p3d_wgrad_tile(p, loc % mw.gx[j], loc / mw.gx[j]);
 }
 
 // =====================================================================================
@@ -1194,6 +1225,7 @@ struct p3d_model {
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
   std::vector<hipEvent_t> gev;   // per-layer gradient-ready events (p3d_grad_events)
+  int wgrad_multi = 1;           // all layers' dW in one k_wgrad_multi launch (env P3D_WGRAD_MULTI)
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
@@ -1416,6 +1448,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
+  if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH5")) m->serve_depth5 = atoi(ev);
@@ -2082,6 +2115,10 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   bool dz_pk = false;         // dy is row-major; every later dz is packed
   int dsel = 0;
   const float* dres_next = nullptr;  // block-output gradient to add when differentiating an A-layer
+  // weight gradients batched into one launch after the loop, unless Adam is fused into them or
+  // per-layer gradient-ready events (bucketed DP all-reduce) need them layer by layer
+  const bool multi = m->wgrad_multi && !m->fuse_adam && m->gev.empty() && nl <= P3D_WG_MULTI;
+  WgradMulti mw{};
   for (int l = nl - 1; l >= 0; --l) {
     const Layer& ly = m->layers[l];
     WgradArgs wa{};
@@ -2100,6 +2137,13 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       if (l >= 1 && m->layers[l - 1].bn) {
         wa.bn_adam = 1; wa.gflat = grads; wa.goff = m->layers[l - 1].gamma; wa.btoff = m->layers[l - 1].beta;
       }
+    } else if (multi) {
+      WgradLayer& w = mw.ly[mw.n];
+      w.X = wa.X; w.dZ = wa.dZ; w.dW = wa.dW; w.db = wa.db; w.ldx = wa.ldx; w.ldz = wa.ldz;
+      w.xpk = wa.xpk; w.zpk = wa.zpk; w.M = wa.M; w.K = wa.K; w.N = wa.N;
+      mw.gx[mw.n] = (wa.N + 63) / 64;
+      mw.begin[mw.n + 1] = mw.begin[mw.n] + mw.gx[mw.n] * ((wa.K + 63) / 64);
+      ++mw.n;
     } else {
       int rc = launch_wgrad(m, wa, st);
       if (rc) return rc;
@@ -2183,6 +2227,11 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[l], st));
     dz_cur = m->dz[l - 1];
     dz_pk = true;
+  }
+  if (multi && mw.n > 0) {
+    ProfScope ps(m, "wgrad_multi");
+    go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+    LAUNCH_CHECK("k_wgrad_multi");
   }
   if (c.max_norm) {
     // G (dL/dW_eff) -> dL/dW through clip_by_norm

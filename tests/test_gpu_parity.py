@@ -402,3 +402,22 @@ def test_bf16_inference_matches_emulated_oracle(L, N, B):
     with pytest.raises(ValueError):
         m.forward_device(torch.from_numpy(x).cuda(), training=True)
     m.close()
+
+
+@pytest.mark.parametrize("max_norm,p14,B", [(False, False, 64), (True, False, 64), (False, True, 37), (False, False, 200)])
+def test_wgrad_multi_bit_identical(max_norm, p14, B, monkeypatch):
+    """All layers' weight gradients in one k_wgrad_multi launch (default) == one k_wgrad
+    launch per layer (P3D_WGRAD_MULTI=0), bit for bit, and the oracle's gradients."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True, max_norm=max_norm,
+                      predict_14=p14)
+    rng = np.random.default_rng(31)
+    x = rng.standard_normal((B, 32))
+    t = rng.standard_normal((B, 42 if p14 else 48))
+    gs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("P3D_WGRAD_MULTI", flag)
+        st, m = make(cfg, batch=B, max_batch=max(B, 64))
+        m.compute_gradients(x, t, 0.5, ctr=5)
+        gs.append(m.flat["grads"].clone())
+        m.close()
+    assert torch.equal(gs[0], gs[1])
