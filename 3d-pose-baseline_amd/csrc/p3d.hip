@@ -882,11 +882,15 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs p) { p3d_wgrad_tile(p, 
 struct WgradLayer {
   const float* X; const float* dZ; float* dW; float* db;
   int64_t ldx, ldz; int xpk, zpk, M, K, N;
+  // fused Adam (WgradArgs): flat offsets of W / b and of the previous layer's gamma / beta,
+  // the layer's packed copies
+  int bn_adam; int64_t woff, boff, goff, btoff; float* wd; float* wf;
 };
 struct WgradMulti {
   int n;
   int begin[P3D_WG_MULTI + 1];   // workgroup prefix over layers
   int gx[P3D_WG_MULTI];          // column tiles of each layer
+  int adam; AdamFuse af; float* w; float* m; float* v; const float* gflat;
   WgradLayer ly[P3D_WG_MULTI];
 };
 __global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
@@ -897,6 +901,11 @@ __global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
   WgradArgs p{};
   p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
   p.M = l.M; p.K = l.K; p.N = l.N; p.dW = l.dW; p.db = l.db;
+  if (mw.adam) {
+    p.adam = 1; p.af = mw.af; p.w = mw.w; p.m = mw.m; p.v = mw.v; p.woff = l.woff; p.boff = l.boff;
+    p.wd = l.wd; p.wf = l.wf;
+    p.bn_adam = l.bn_adam; p.gflat = mw.gflat; p.goff = l.goff; p.btoff = l.btoff;
+  }
   const int loc = b - mw.begin[j];
   p3d_wgrad_tile(p, loc % mw.gx[j], loc / mw.gx[j]);
 }
@@ -1171,7 +1180,7 @@ struct p3d_model {
   int nlossp = 0;
   float* loss_dst = nullptr;  // set during p3d_train_fwd_bwd: the backward folds the loss here
   const AdamFuse* fuse_adam = nullptr;  // set during p3d_train_step: Adam fused into the backward
-  int adam_in_wgrad = 0;      // env P3D_FUSE_ADAM=1: p3d_train_step applies Adam inside k_wgrad
+  int adam_in_wgrad = 1;      // env P3D_FUSE_ADAM (default 1): p3d_train_step applies Adam inside k_wgrad_multi
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
@@ -2117,8 +2126,24 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   const float* dres_next = nullptr;  // block-output gradient to add when differentiating an A-layer
   // weight gradients batched into one launch after the loop, unless Adam is fused into them or
   // per-layer gradient-ready events (bucketed DP all-reduce) need them layer by layer
-  const bool multi = m->wgrad_multi && !m->fuse_adam && m->gev.empty() && nl <= P3D_WG_MULTI;
+  const bool multi = m->wgrad_multi && m->gev.empty() && nl <= P3D_WG_MULTI;
   WgradMulti mw{};
+  if (m->fuse_adam) {
+    mw.adam = 1; mw.af = *m->fuse_adam; mw.w = m->flat[0]; mw.m = m->flat[2]; mw.v = m->flat[3]; mw.gflat = grads;
+  }
+  // a layer's weight gradient (+ fused Adam): into the batched launch, or launched now
+  auto emit = [&](const WgradArgs& wa) -> int {
+    if (!multi) return launch_wgrad(m, wa, st);
+    WgradLayer& w = mw.ly[mw.n];
+    w.X = wa.X; w.dZ = wa.dZ; w.dW = wa.dW; w.db = wa.db; w.ldx = wa.ldx; w.ldz = wa.ldz;
+    w.xpk = wa.xpk; w.zpk = wa.zpk; w.M = wa.M; w.K = wa.K; w.N = wa.N;
+    w.bn_adam = wa.bn_adam; w.woff = wa.woff; w.boff = wa.boff; w.goff = wa.goff; w.btoff = wa.btoff;
+    w.wd = wa.wd; w.wf = wa.wf;
+    mw.gx[mw.n] = (wa.N + 63) / 64;
+    mw.begin[mw.n + 1] = mw.begin[mw.n] + mw.gx[mw.n] * ((wa.K + 63) / 64);
+    ++mw.n;
+    return P3D_OK;
+  };
   for (int l = nl - 1; l >= 0; --l) {
     const Layer& ly = m->layers[l];
     WgradArgs wa{};
@@ -2137,20 +2162,13 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       if (l >= 1 && m->layers[l - 1].bn) {
         wa.bn_adam = 1; wa.gflat = grads; wa.goff = m->layers[l - 1].gamma; wa.btoff = m->layers[l - 1].beta;
       }
-    } else if (multi) {
-      WgradLayer& w = mw.ly[mw.n];
-      w.X = wa.X; w.dZ = wa.dZ; w.dW = wa.dW; w.db = wa.db; w.ldx = wa.ldx; w.ldz = wa.ldz;
-      w.xpk = wa.xpk; w.zpk = wa.zpk; w.M = wa.M; w.K = wa.K; w.N = wa.N;
-      mw.gx[mw.n] = (wa.N + 63) / 64;
-      mw.begin[mw.n + 1] = mw.begin[mw.n] + mw.gx[mw.n] * ((wa.K + 63) / 64);
-      ++mw.n;
     } else {
-      int rc = launch_wgrad(m, wa, st);
+      int rc = emit(wa);
       if (rc) return rc;
     }
     if (l == 0) {
       if (fuse) {
-        int rc = launch_wgrad(m, wa, st);
+        int rc = emit(wa);
         if (rc) return rc;
       }
       if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[0], st));
@@ -2220,7 +2238,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     }
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
     if (fuse) {
-      int rc = launch_wgrad(m, wa, st);
+      int rc = emit(wa);
       if (rc) return rc;
     }
     // layer l's W and b (wgrad above) and its gamma/beta (bn_bwd of iteration l + 1) are final

@@ -455,15 +455,18 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         # single GPU (p3d_train_step): Adam runs inside the weight-gradient kernels; per step
         # they read X and dZ, read+write W, m, v, write Wf, Wd (4 B each), and update the
         # biases and the previous layer's BN gamma/beta (read+write w, m, v)
-        cnt, avg_us, _, _ = prof["wgrad"]
         shapes = [(IN, L)] + [(L, L)] * (2 * NBLK) + [(L, OUT)]
         byts = sum(4 * (BATCH * K + BATCH * N) + 4 * 8 * K * N + 4 * 6 * N for K, N in shapes)
         byts += 4 * 12 * L * (2 * NBLK + 1)          # gamma, beta of every BN layer
-        per_step = len(shapes)
+        multi = "wgrad_multi" in prof                # all layers in one launch (default)
+        cnt, avg_us, _, _ = prof["wgrad_multi" if multi else "wgrad"]
+        per_step = 1 if multi else len(shapes)
         achieved = byts / (per_step * avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _committed_traffic("k_wgrad"),
-                "kernel": "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": _committed_traffic("k_wgrad_multi" if multi else "k_wgrad"),
+                "kernel": ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
+                           if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step),
                 "bytes_per_step": int(byts), "avg_us": round(avg_us, 3), "launches_timed": cnt}
     roof["event_pair_avg_us"] = {k: round(v[1], 3) for k, v in prof.items()}
     model.close()

@@ -150,10 +150,11 @@ int p3d_layer_grad_range(const p3d_model* m, int32_t layer, int64_t* begin, int6
 int p3d_stream_wait_grad(p3d_model* m, int32_t layer, void* stream);
 
 /* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
- * the TF1 Adam update, global_step += 1.  With env P3D_FUSE_ADAM=1 at p3d_create the update
- * runs inside the weight-gradient kernels instead (no separate optimizer pass; the flat
- * grads buffer then holds the bias and BN gradients, not dW), bit-identical to the unfused
- * sequence (tests/test_gpu_parity.py) but slower at cfg3.
+ * the TF1 Adam update, global_step += 1.  By default (env P3D_FUSE_ADAM=1 at p3d_create) the
+ * update runs inside the batched weight-gradient launch (k_wgrad_multi: no separate optimizer
+ * pass; the flat grads buffer then holds the bias and BN gradients, not dW), bit-identical to
+ * the unfused sequence (tests/test_gpu_parity.py) and faster at cfg3;
+ * P3D_FUSE_ADAM=0 runs k_adam_pack after the backward.
  * lr = lr0 * decay_rate^(global_step / decay_steps) on the device.  Equivalent to
  * p3d_train_fwd_bwd + p3d_adam_step_decay (which --max_norm models use internally).
  * Graph-capturable; data-parallel training uses the unfused calls around its all-reduce. */
