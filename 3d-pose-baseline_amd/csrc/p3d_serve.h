@@ -40,6 +40,9 @@
 #define P3D_SERVE_MAXL 16          // input + 2*blocks + output layers
 // layers whose epilogue constants k_serve5 keeps in LDS (input + hidden): 15, or 9 (N <= 4
 // blocks) for the 8-column-tile form, whose K-combine buffer takes 128 KB
+#ifndef P3D_SERVE_IN_EARLY
+#define P3D_SERVE_IN_EARLY 0       // next step's input-layer operands requested after the K-combine
+#endif
 #ifndef P3D_S4_RE                  // 8-column-tile form (SPLIT 4, UPM 4) variants
 #define P3D_S4_RE 2                // output-reduction elements per lane
 #endif
@@ -924,6 +927,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         __syncthreads();
         P3D_SERVE_STAMP(tr, 4);
+        // (P3D_SERVE_IN_EARLY) the next step's first input-layer operands requested here, the
+        // K-slice accumulators being dead: their latency hides under the epilogue and the
+        // fused output-layer partials
+        InOps nx_early;
+        if (P3D_SERVE_IN_EARLY && UPM < 4 && in_now) in_load(uu[0], row0 + (int64_t)ng * 64, nx_early);
         if (red_here && split_red && first_u && tid < ecnt) {
           f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -986,7 +994,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         } else if (in_now) {
           InOps nx;
-          in_load(uu[0], row0 + (int64_t)ng * 64, nx);
+          if (P3D_SERVE_IN_EARLY && UPM < 4) nx = nx_early;
+          else in_load(uu[0], row0 + (int64_t)ng * 64, nx);
           in_finish(uu[0], nx, c0n);
 #pragma unroll
           for (int k = 1; k < UPM; ++k)
