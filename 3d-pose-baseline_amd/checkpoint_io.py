@@ -29,8 +29,23 @@ def trainable_order(param_table):
 
 
 def global_order(param_table):
-    """tf.global_variables() names of the reference graph, in creation order."""
-    names = ["learning_rate", "global_step"] + [n for n, _, _, _ in param_table]
+    """tf.global_variables() names of the reference graph, in creation order.
+
+    ``tf.layers.batch_normalization`` creates gamma, beta, moving_mean, moving_variance in
+    that order inside its scope (src/linear_model.py:112,181,193), so each BN scope's moving
+    statistics follow its beta -- whatever order the param table (p3d_create lists every
+    moving statistic after all trainables) uses."""
+    moving = {}
+    for n, _, kind, _ in param_table:
+        if kind != 0:
+            moving.setdefault(n.rsplit("/", 1)[0], []).append(n)
+    names = ["learning_rate", "global_step"]
+    for n in trainable_order(param_table):
+        names.append(n)
+        if n.endswith("/beta"):
+            names += moving.pop(n.rsplit("/", 1)[0], [])
+    for rest in moving.values():       # moving statistics of a scope without beta (none in TF1)
+        names += rest
     names += ["beta1_power", "beta2_power"]
     for n in trainable_order(param_table):
         names += [n + "/Adam", n + "/Adam_1"]

@@ -79,8 +79,9 @@ class Summary:
 class SummaryWriter:
     """tf.summary.FileWriter stand-in: appends JSON lines to <dir>/events.jsonl."""
 
-    def __init__(self, logdir):
+    def __init__(self, logdir, enabled=True):
         self.logdir = logdir
+        self.enabled = enabled   # data parallel: only rank 0 writes events
         self._path = None
 
     def _file(self):
@@ -90,6 +91,8 @@ class SummaryWriter:
         return self._path
 
     def add_summary(self, summary, global_step=None):
+        if not self.enabled:
+            return
         items = summary if isinstance(summary, (list, tuple)) else [summary]
         with open(self._file(), "a") as f:
             for s in items:
@@ -128,8 +131,13 @@ class Saver:
         self._saved = []
 
     def save(self, session, save_path, global_step=None):
+        """Collective under data parallelism: every rank calls it (the moving statistics are
+        averaged over the replicas), rank 0 alone writes, and the ranks leave together."""
         path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
         self.model.sync_moving_stats()   # data parallel: one set of moving statistics
+        if self.model.rank != 0:
+            self._barrier()
+            return path
         state = self.model.get_state()
         d = os.path.dirname(path)
         if d:
@@ -142,7 +150,13 @@ class Saver:
             old = self._saved.pop(0)
             if os.path.exists(old + ".npz"):
                 os.remove(old + ".npz")
+        self._barrier()
         return path
+
+    def _barrier(self):
+        if self.model.data_parallel:
+            import torch.distributed as dist
+            dist.barrier()
 
     def save_npy_dump(self, session, directory, all_variables=False):
         """The reference's per-variable npy export (src/predict_3dpose.py:548-568)."""
@@ -213,12 +227,6 @@ class LinearModel(object):
         self.err_mm = Placeholder("error_mm")
         self.err_mm_summary = ("summary", "loss/error_mm")
         self.outputs = "outputs"
-        self.train_writer = SummaryWriter(os.path.join(summaries_dir, "train"))
-        self.test_writer = SummaryWriter(os.path.join(summaries_dir, "test"))
-        self.global_step = _Scalar(lambda: self.get_step()[0])
-        self.learning_rate = _Scalar(lambda: exponential_decay(self.lr0, self.get_step()[0]))
-        self.saver = Saver(self, max_to_keep=10)
-
         # data parallelism (pure DP over RCCL; see dist.py / DESIGN.md)
         import torch.distributed as dist
         if data_parallel is None:
@@ -226,6 +234,12 @@ class LinearModel(object):
         self.data_parallel = bool(data_parallel)
         self.rank = dist.get_rank() if self.data_parallel else 0
         self.world = dist.get_world_size() if self.data_parallel else 1
+
+        self.train_writer = SummaryWriter(os.path.join(summaries_dir, "train"), enabled=self.rank == 0)
+        self.test_writer = SummaryWriter(os.path.join(summaries_dir, "test"), enabled=self.rank == 0)
+        self.global_step = _Scalar(lambda: self.get_step()[0])
+        self.learning_rate = _Scalar(lambda: exponential_decay(self.lr0, self.get_step()[0]))
+        self.saver = Saver(self, max_to_keep=10)
 
         self._loss_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._step_host = 0   # host mirror of the device global_step (step() summaries, no sync)

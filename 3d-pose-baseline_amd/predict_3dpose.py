@@ -51,6 +51,16 @@ def build_parser():
     p.add_argument("--cameras_path", type=str, default="data/h36m/cameras.h5", help="Directory to load camera parameters")
     p.add_argument("--data_dir", type=str, default="data/h36m/", help="Data directory")
     p.add_argument("--train_dir", type=str, default="experiments", help="Training directory.")
+    # openpose front ends (src/predict_3dpose.py:76-91; read by src/openpose_3dpose_sandbox.py:240-446)
+    p.add_argument("--pose_estimation_json", type=str, default="/tmp/",
+                   help="pose estimation json output directory, openpose or tf-pose-estimation")
+    p.add_argument("--interpolation", action='store_true', default=False, help="interpolate openpose json")
+    p.add_argument("--multiplier", type=float, default=0.1, help="interpolation frame range")
+    p.add_argument("--write_gif", action='store_true', default=False, help="write final anim gif")
+    p.add_argument("--gif_fps", type=int, default=30, help="output gif framerate")
+    p.add_argument("--verbose", type=int, default=2, help="0:Error, 1:Warning, 2:INFO*(default), 3:debug")
+    p.add_argument("--cache_on_fail", action='store_true', default=True,
+                   help="caching last valid frame on invalid frame")
     p.add_argument("--sample", action='store_true', default=False, help="Set to True for sampling.")
     p.add_argument("--use_cpu", action='store_true', default=False, help="Whether to use the CPU")
     p.add_argument("--load", type=int, default=0, help="Try to load a previous checkpoint.")
@@ -59,6 +69,9 @@ def build_parser():
     p.add_argument("--synthetic", action='store_true', default=False,
                    help="Use synthetic H3.6M-shaped data (the dataset is not part of this build)")
     p.add_argument("--seed", type=int, default=0, help="Weight / dropout seed")
+    p.add_argument("--max_batch", type=int, default=8192,
+                   help="rows the device workspaces hold (evaluation submits up to this many rows per "
+                        "launch); front ends stepping single frames can pass their batch size")
     p.add_argument("--device_loop", type=int, default=1,
                    help="1: stage each epoch in HBM and train without per-step host round trips; "
                         "0: the reference's per-batch step() loop")
@@ -115,7 +128,7 @@ def create_model(session, actions, batch_size, flags=None):
     model = linear_model.LinearModel(flags.linear_size, flags.num_layers, flags.residual, flags.batch_norm,
                                      flags.max_norm, batch_size, flags.learning_rate,
                                      os.path.join(tdir, "log"), flags.predict_14, seed=flags.seed,
-                                     max_batch=max(batch_size, 8192))
+                                     max_batch=max(batch_size, getattr(flags, "max_batch", 8192)))
     if flags.load <= 0:
         print("Creating model with fresh parameters.")
         return model
@@ -306,6 +319,13 @@ def synthetic_h36m(n_train=20000, n_test=4000, seed=0, out_dim=48):
                 data_std_2d=std2, dim_to_use_2d=use2, dim_to_ignore_2d=ign2)
 
 
+def dp_epoch_share(enc, dec, rank, world):
+    """This rank's batches of a data-parallel epoch: equal contiguous shares of the
+    (identically permuted) batch list, so every replica runs the same number of steps."""
+    per = len(enc) // world
+    return enc[rank * per:(rank + 1) * per], dec[rank * per:(rank + 1) * per]
+
+
 def load_data(flags):
     if flags.synthetic:
         return synthetic_h36m(out_dim=42 if flags.predict_14 else 48, seed=flags.seed)
@@ -327,8 +347,16 @@ def train(flags=None):
         current_step = 0 if flags.load <= 0 else flags.load + 1
         log_every_n_batches = 100
         for epoch in range(1, flags.epochs + 1):
+            if model.data_parallel:
+                # one epoch covers the training set once over all replicas: every rank draws the
+                # same permutation and trains on its own equal share of the batches (the global
+                # batch is world x batch_size; a remainder of < world batches is dropped, like
+                # the reference's n % batch_size tail)
+                np.random.seed((flags.seed * 1000003 + epoch) % (2 ** 32))
             enc, dec = model.get_all_batches(d["train_set_2d"], d["train_set_3d"], flags.camera_frame,
                                              training=True)
+            if model.data_parallel:
+                enc, dec = dp_epoch_share(enc, dec, model.rank, model.world)
             nbatches = len(enc)
             print("There are {0} train batches".format(nbatches))
             start_time, loss = time.time(), 0.

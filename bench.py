@@ -51,6 +51,26 @@ def flops_per_pose(L=L, N=NBLK):
     return 2 * (IN * L + 2 * N * L * L + OUT * L)
 
 
+def launch_ranks(n, dry=False):
+    """`bench.py --gpus N` outside a launcher: run N ranks of this script under
+    torch.distributed.run (127.0.0.1 rendezvous, a free port) as a child process and
+    return its exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    if dry:
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
 def setup_dist():
     import torch
     import torch.distributed as dist
@@ -130,29 +150,35 @@ def kernel_name(model, what):
     return buf.value.decode()
 
 
-def _committed_traffic(symbol):
-    """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC summary
-    (profiles/*pmc_traffic*.json, FETCH_SIZE x2 + WRITE_SIZE; see tools/pmc_traffic.py)."""
+def _pmc_files(config):
+    """Committed rocprofv3 PMC summaries (profiles/*pmc_traffic*.json, FETCH_SIZE x2 +
+    WRITE_SIZE; tools/pmc_traffic.py) measured on the configuration this run uses: every
+    entry of `config` must equal the file's "__config__" (newest file first).  A figure
+    measured on another configuration (e.g. 1000 steps per launch instead of 20) is never
+    reported as this run's traffic."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
             continue
+        have = d.get("__config__", {})
+        if all(have.get(k) == v for k, v in config.items()):
+            yield {k: v for k, v in d.items() if k != "__config__"}
+
+
+def _committed_traffic(symbol, config):
+    """HBM bytes per launch of `symbol` on `config` (see _pmc_files), or None."""
+    for d in _pmc_files(config):
         for k, v in d.items():
             if symbol in k:
                 return v["hbm_bytes_per_launch"]
     return None
 
 
-def _committed_traffic_avg(symbol):
+def _committed_traffic_avg(symbol, config):
     """Launch-weighted mean HBM bytes per launch over every committed kernel matching `symbol`."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
-        try:
-            d = json.load(open(f))
-        except Exception:
-            continue
+    for d in _pmc_files(config):
         hits = [v for k, v in d.items() if symbol in k]
         if hits:
             n = sum(v["launches"] for v in hits)
@@ -277,7 +303,8 @@ def bench_serve(args, rank, world):
     flop = float(C * BATCH * flops_per_pose())
     achieved = flop / (avg_us * 1e-6) / 1e12
     kname = kernel_name(model, 3)
-    traffic = args.traffic if args.traffic is not None else _committed_traffic(kname)
+    traffic = args.traffic if args.traffic is not None else \
+        _committed_traffic(kname, {"mode": "infer", "steps_per_launch": C})
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "kernel": kname + " (persistent: %d batch-64 steps per launch, whole network per XCD, fp32 MFMA 16x16x4)" % C,
@@ -380,7 +407,7 @@ def bench_infer(args, rank, world):
     flop = 2.0 * BATCH * L * L          # one hidden-layer launch: [64,1024] x [1024,1024]
     achieved = flop / (avg_us * 1e-6) / 1e12
     kname = kernel_name(model, 0)
-    traffic = args.traffic if args.traffic is not None else _committed_traffic(kname)
+    traffic = _committed_traffic(kname, {"mode": "chain", "batch": BATCH})
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "kernel": kname + " (hidden Linear+BN+ReLU+residual, fp32 MFMA 16x16x4)",
@@ -449,7 +476,7 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         byts = 7 * 4 * n_params + 2 * 4 * n_w
         achieved = byts / (avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _committed_traffic("k_adam_pack"),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _committed_traffic("k_adam_pack", {"mode": "train", "batch": BATCH}),
                 "kernel": "k_adam_pack", "bytes_per_launch": byts, "avg_us": round(avg_us, 3)}
     else:
         # single GPU (p3d_train_step): Adam runs inside the weight-gradient kernels; per step
@@ -464,7 +491,8 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         achieved = byts / (per_step * avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": _committed_traffic("k_wgrad_multi" if multi else "k_wgrad"),
+                "traffic": _committed_traffic("k_wgrad_multi" if multi else "k_wgrad",
+                                              {"mode": "train", "batch": BATCH}),
                 "kernel": ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
                            if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step),
                 "bytes_per_step": int(byts), "avg_us": round(avg_us, 3), "launches_timed": cnt}
@@ -545,7 +573,7 @@ def bench_eval(args, rank, world):
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_PEAK_TFLOPS, 4),
                 "kernel": kernel_name(model, 1) + " (hidden layers, %d-row launches)" % chunk,
-                "traffic": _committed_traffic(kernel_name(model, 1)),
+                "traffic": _committed_traffic(kernel_name(model, 1), {"mode": "eval", "chunk": chunk}),
                 "flop_per_launch": int(flop / cnt), "avg_us": round(avg_us, 3), "launches_timed": cnt}
     else:
         roof = None
@@ -665,7 +693,7 @@ def bench_stress(args, rank, world):
     flop = 2.0 * Bs * Ls * Ls
     achieved = flop / (avg_us * 1e-6) / 1e12
     roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16p<64, 4, 8, false>"),
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16p<64, 4, 8, false>", {"mode": "stress", "batch": Bs}),
             "kernel": "k_gemm_bf16p<64, 4, 8, false> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
             "isolated_avg_us": round(iso_us, 3)}
@@ -759,7 +787,7 @@ def bench_data(args, rank, world):
     nbytes = (2 * F2 * 64 * 8 + 2 * F2 * 96 * 8) / 4
     t_ms = (ms("moments2_0", "moments2_1") + ms("moments3_0", "moments3_1")) / 4
     ach = nbytes / (t_ms * 1e-3) / 1e9
-    traffic = _committed_traffic_avg("k_col_partial")
+    traffic = _committed_traffic_avg("k_col_partial", {"mode": "data", "frames": S * frames})
     out = {"workload": "H3.6M train-set preprocessing (create_2d_data + read_3d_data numerics), "
                        "%d world frames x 4 cameras, float64" % (S * frames),
            "value": round(F2 / dt, 1), "unit": "camera-poses/s", "ms_per_pass": round(1000.0 * dt, 3),
@@ -831,10 +859,17 @@ def main():
     ap.add_argument("--data-reps", type=int, default=10)
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the N-rank launch command --gpus N > 1 would run, and exit")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start N fresh ranks and wait for them.  This process touches
+        # no GPU (never re-exec a process that has initialised one).
+        return launch_ranks(args.gpus, dry=args.launch_dry_run)
+    if args.gpus != int(os.environ.get("WORLD_SIZE", "1")):
+        raise SystemExit("bench.py: --gpus %d but the job has %s rank(s) (WORLD_SIZE)"
+                         % (args.gpus, os.environ.get("WORLD_SIZE", "1")))
     rank, world, local = setup_dist()
-    if args.gpus != world and world > 1:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     train = single = sweep = api = data = None
     chain = None
     if args.mode == "infer":
@@ -944,7 +979,11 @@ def main():
 
 if __name__ == "__main__":
     try:
-        main()
+        rc = main()
+        if rc:
+            sys.exit(rc)
+    except SystemExit:
+        raise
     except BaseException:
         # report and leave without interpreter teardown: unwinding with live HIP graphs and
         # streams after an exception has crashed the process (SIGSEGV) on the box

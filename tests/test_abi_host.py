@@ -133,6 +133,19 @@ def test_flags_defaults_follow_reference():
                              "batch_normalization", "not_stacked_hourglass", "predict_17")
 
 
+def test_flags_include_openpose_frontend_flags():
+    """src/openpose_3dpose_sandbox.py:240-446 reads these through `from predict_3dpose import
+    FLAGS`; names and defaults of src/predict_3dpose.py:76-91."""
+    f = predict_3dpose.FLAGS
+    assert (f.pose_estimation_json, f.interpolation, f.multiplier) == ("/tmp/", False, 0.1)
+    assert (f.write_gif, f.gif_fps, f.verbose, f.cache_on_fail) == (False, 30, 2, True)
+    g = predict_3dpose.build_parser().parse_args(["--interpolation", "--multiplier", "0.5", "--write_gif",
+                                                  "--gif_fps", "10", "--verbose", "3",
+                                                  "--pose_estimation_json", "/data/json/"])
+    assert (g.interpolation, g.multiplier, g.write_gif, g.gif_fps, g.verbose) == (True, 0.5, True, 10, 3)
+    assert g.pose_estimation_json == "/data/json/"
+
+
 def test_model_requires_gpu():
     import torch
     if torch.cuda.is_available():
@@ -170,6 +183,32 @@ def test_checkpoint_io_names_and_order():
     assert cio.parse_dump_filename("notes.txt") is None
 
 
+def test_checkpoint_global_order_library_table():
+    """The table as p3d_create lays it out (every trainable, then every moving statistic):
+    tf.global_variables() still puts each BN scope's moving_mean / moving_variance right
+    after its beta (src/linear_model.py:112,181,193; the dump of src/predict_3dpose.py:559-568)."""
+    import checkpoint_io as cio
+    bn = ["linear_model/batch_normalization", "linear_model/two_linear_0/batch_normalization10",
+          "linear_model/two_linear_0/batch_normalization20"]
+    table = [("linear_model/w1", 8192, 0, 0), ("linear_model/b1", 256, 0, 0),
+             (bn[0] + "/gamma", 256, 0, 0), (bn[0] + "/beta", 256, 0, 0),
+             ("linear_model/two_linear_0/w2_0", 65536, 0, 0), ("linear_model/two_linear_0/b2_0", 256, 0, 0),
+             (bn[1] + "/gamma", 256, 0, 0), (bn[1] + "/beta", 256, 0, 0),
+             ("linear_model/two_linear_0/w3_0", 65536, 0, 0), ("linear_model/two_linear_0/b3_0", 256, 0, 0),
+             (bn[2] + "/gamma", 256, 0, 0), (bn[2] + "/beta", 256, 0, 0),
+             ("linear_model/w4", 12288, 0, 0), ("linear_model/b4", 48, 0, 0)]
+    for s in bn:
+        table += [(s + "/moving_mean", 256, 1, 0), (s + "/moving_variance", 256, 1, 0)]
+    g = cio.global_order(table)
+    for s in bn:
+        i = g.index(s + "/beta")
+        assert g[i - 1] == s + "/gamma"
+        assert g[i + 1:i + 3] == [s + "/moving_mean", s + "/moving_variance"]
+    assert g.index("linear_model/w4") == g.index(bn[2] + "/moving_variance") + 1
+    assert len(g) == 2 + len(table) + 2 + 2 * 14
+    assert g.index("beta1_power") == 2 + len(table)
+
+
 def test_openpose_mapping_matches_oracle():
     """Host joint mapping of the OpenPose front end (src/openpose_3dpose_sandbox.py:25,326-342)."""
     import openpose_frontend
@@ -180,3 +219,17 @@ def test_openpose_mapping_matches_oracle():
     for i in range(7):
         np.testing.assert_array_equal(got[i], ref_frontend.map_frame(frames[i]))
     assert openpose_frontend.ORDER == ref_frontend.ORDER
+
+
+def test_dp_epoch_share_equal_disjoint():
+    """Data-parallel epoch: equal contiguous shares of one shared batch list (every replica
+    runs the same number of steps; < world leftover batches dropped)."""
+    enc = [np.full((2, 32), i) for i in range(11)]
+    dec = [np.full((2, 48), i) for i in range(11)]
+    seen = []
+    for r in range(3):
+        e, d = predict_3dpose.dp_epoch_share(enc, dec, r, 3)
+        assert len(e) == len(d) == 3
+        assert [int(a[0, 0]) for a in e] == [int(a[0, 0]) for a in d]
+        seen += [int(a[0, 0]) for a in e]
+    assert seen == list(range(9))

@@ -277,6 +277,14 @@ def test_npy_dump_round_trip(tmp_path):
     paths = m.saver.save_npy_dump(None, str(tmp_path / "all"), all_variables=True)
     m.saver.save_npy_dump(None, str(tmp_path / "tr"))
     assert os.path.basename(paths[2]) == "0002 - linear_model-w1:0.npy"
+    # tf.global_variables(): each BN scope's moving statistics right after its beta
+    names = [checkpoint_io.parse_dump_filename(p)[1] for p in paths]
+    for s in ("linear_model/batch_normalization", "linear_model/two_linear_0/batch_normalization10",
+              "linear_model/two_linear_0/batch_normalization20"):
+        i = names.index(s + "/beta")
+        assert names[i + 1:i + 3] == [s + "/moving_mean", s + "/moving_variance"], names[i - 1:i + 4]
+    assert names.index("linear_model/w4") == names.index("linear_model/two_linear_0/batch_normalization20"
+                                                         "/moving_variance") + 1
     full = m.get_state()
     _, m2 = make(cfg, model_seed=99)
     loaded = m2.saver.restore_npy_dump(None, str(tmp_path / "all"))
