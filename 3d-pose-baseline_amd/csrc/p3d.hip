@@ -20,6 +20,7 @@
 #include "p3d_gemm.h"
 #include "p3d_data.h"
 #include "p3d_serve.h"
+#include "p3d_serve6.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -1225,6 +1226,7 @@ struct p3d_model {
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
+  float* serve_ec = nullptr;   // k_serve6 epilogue constants (k_serve_prep, every launch)
   unsigned* serve_sync = nullptr;
   int* serve_err = nullptr;
   int serve_grid = 0;
@@ -1236,6 +1238,11 @@ struct p3d_model {
   std::vector<hipEvent_t> gev;   // per-layer gradient-ready events (p3d_grad_events)
   int wgrad_multi = 1;           // all layers' dW in one k_wgrad_multi launch (env P3D_WGRAD_MULTI)
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
+  int serve6 = 1;           // k_serve6 for launches of <= serve6_max_nb steps (env P3D_SERVE6: 0 off, 1 auto, 2 always)
+  int serve6_max_nb = 32;   // (env P3D_SERVE6_MAX_NB)
+  int serve6_split = 0;     // k_serve6 groups per XCD, 0 = chosen per launch (env P3D_SERVE6_SPLIT: 1..4)
+  int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
+  std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -1283,6 +1290,7 @@ void free_all(p3d_model* m) {
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
+  if (m->serve_ec) (void)hipFree(m->serve_ec);
 }
 }  // namespace
 
@@ -1466,6 +1474,10 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_SERVE_SPLIT")) m->serve_split = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_UPM")) m->serve_upm = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6")) m->serve6 = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6_MAX_NB")) m->serve6_max_nb = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6_SPLIT")) m->serve6_split = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6_DEPTH")) m->serve6_depth = atoi(ev);
   {
     StepState s0{};
     s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
@@ -1974,6 +1986,53 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
   }
 }
 
+// ---- k_serve6 (p3d_serve6.h): launches of a few dozen steps ----------------------------
+// Groups per XCD for nb steps: the S minimising (rounds of steps) x (fixed cost per phase +
+// cost per column tile x tiles per CU), with 32 CUs per XCD (grid / 8): a phase's fixed cost
+// (hand-off, ring fill, K-combine, epilogue) ~4 us, a column tile of K = 1024 ~3.9 us
+// (round-1 phase traces).  nb = 20 -> S = 3 (all steps at once, <= 7 tiles per
+// CU); nb <= 8 -> S = 1; nb = 16 -> S = 2.
+static int serve6_split_for(const p3d_model* m, int64_t nb, int T) {
+  if (m->serve6_split >= 1 && m->serve6_split <= 4) return m->serve6_split;
+  const int cx = std::max(1, m->serve_grid / 8);
+  const double cfix = 4.0, ctile = 3.9 * T / 64.0;
+  int best = 1;
+  double bt = 1e30;
+  for (int S = 1; S <= 4; ++S) {
+    const int nmin = cx / S;
+    if (nmin < 1) break;
+    const double rounds = (double)((nb + 8 * S - 1) / (8 * S));
+    const double t = rounds * (cfix + ctile * ((T + nmin - 1) / nmin));
+    if (t < bt - 1e-9) { bt = t; best = S; }
+  }
+  return best;
+}
+
+// column tiles per contraction: the smallest built form covering a member of the smallest group
+static int serve6_ncm(const p3d_model* m, int S, int T) {
+  const int nmin = std::max(1, std::max(1, m->serve_grid / 8) / S);
+  const int need = (T + nmin - 1) / nmin;
+  return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : 8;
+}
+
+static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, unsigned grid, hipStream_t st,
+                          const ServeArgs& a) {
+  // ring depth 4 for the narrow forms; 2 for 7 / 8 tiles (depth 4 spills there: 77 / 136
+  // registers; depth 2 none / 38)
+  if (ncm == 2) {
+    if (depth == 4) go(ps, k_serve6<4, 3, 2>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_serve6<2, 3, 2>, dim3(grid), dim3(256), st, a);
+  } else if (ncm == 4) {
+    if (depth == 4) go(ps, k_serve6<4, 3, 4>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_serve6<2, 3, 4>, dim3(grid), dim3(256), st, a);
+  } else if (ncm == 7) {
+    if (depth == 4) go(ps, k_serve6<4, 3, 7>, dim3(grid), dim3(256), st, a);   // weights 4 ahead (53 spills)
+    else go(ps, k_serve6<2, 3, 7>, dim3(grid), dim3(256), st, a);
+  } else {
+    go(ps, k_serve6<2, 3, 8>, dim3(grid), dim3(256), st, a);
+  }
+}
+
 extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream) {
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_serve: null argument");
   const p3d_cfg& c = m->cfg;
@@ -1994,7 +2053,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     m->serve_grid = cus;   // one 512-thread workgroup per CU (the LDS ring admits one)
-    const int64_t nbuf = P3D_SERVE_GROUPS * 3 * slab + P3D_SERVE_GROUPS * 2 * (int64_t)U * PT;
+    // output partials: k_serve5 keeps one per 32-column unit (U), k_serve6 one per 16-column tile (2U)
+    const int64_t nbuf = P3D_SERVE_GROUPS * 3 * slab + P3D_SERVE_GROUPS * 2 * (int64_t)(2 * U) * PT;
     if ((e = hipMalloc(&m->serve_buf, nbuf * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     if ((e = hipMemset(m->serve_buf, 0, nbuf * sizeof(float))) != hipSuccess)
@@ -2004,6 +2064,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if ((e = hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     m->serve_err = (int*)(m->serve_sync + P3D_SERVE_SYNC_WORDS);
+    if ((e = hipMalloc(&m->serve_ec, (size_t)P3D_SERVE_MAXL * L * 3 * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
   }
   ServeArgs a{};
   a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);
@@ -2022,9 +2084,26 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     }
     s.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
   }
-  if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
+  const bool use6 = m->serve6 && c.num_layers > 0 && NDT == 3 &&
+                    (m->serve6 == 2 || a.nb <= (int64_t)m->serve6_max_nb);
+  if (use6) {
+    // one prologue launch: sync words zeroed + epilogue constants formed (k_serve_prep)
+    a.ec = m->serve_ec;
+    const int nwork = std::max(P3D_SERVE_SYNC_WORDS, (2 * c.num_layers + 1) * L);
+    hipLaunchKernelGGL(k_serve_prep, dim3((nwork + 255) / 256), dim3(256), 0, st, a, m->serve_ec);
+  } else if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess) {
     return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-  {
+  }
+  if (use6) {
+    const int T = L / 16;
+    a.split = serve6_split_for(m, a.nb, T);
+    const int ncm = serve6_ncm(m, a.split, T);
+    const int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
+    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ">";
+    ProfScope ps(m, "serve");
+    launch_serve6(ps, m, ncm, depth, (unsigned)m->serve_grid, st, a);
+  } else {
+    m->serve_kname.clear();
     ProfScope ps(m, "serve");
     const unsigned grid = (unsigned)m->serve_grid;
     if (NDT == 1) launch_serve_k<1>(ps, m, grid, st, a);
@@ -2042,7 +2121,12 @@ extern "C" int p3d_serve_check(p3d_model* m) {
   int v = 0;
   hipError_t e = hipMemcpy(&v, m->serve_err, sizeof(int), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
-  if (v) return fail(P3D_ERR_HIP, "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
+  if (v) {
+    // reported once: the word and the sync words are cleared, so later launches are judged
+    // on their own (every launch re-zeroes the sync words before it starts anyway)
+    hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned));
+    return fail(P3D_ERR_HIP, "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
+  }
   return P3D_OK;
 }
 
@@ -2446,6 +2530,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     }
   } else if (what == 1) {
     n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
+  } else if (what == 3 && !m->serve_kname.empty()) {
+    n = m->serve_kname;     // the kernel the last p3d_serve launched
   } else if (what == 3) {
     const int ndt = (m->cfg.output_size + 15) / 16, ks = m->serve_ks == 4 ? 4 : 8;
     if (m->serve_w4 == 5 && m->cfg.num_layers > 0)

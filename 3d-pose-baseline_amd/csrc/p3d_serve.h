@@ -53,7 +53,12 @@
 #define P3D_S4_INPIPE 0            // next unit's input-layer operands during this unit's layer
 #endif
 #define P3D_SERVE_ECL(NC) ((NC) >= 8 ? 9 : P3D_SERVE_MAXL - 1)
-#define P3D_SERVE_SYNC_WORDS 2112  // [0..7] census, [8] arrivals, [64 + 64*g + r] flag of member r of group g
+// sync words: [32 x] census counter of XCD x (a 128-B line each: the 32 arrivals of an XCD
+// serialise on their own line, the 8 XCDs' in parallel -- one counter for all 256 workgroups
+// serialised 256 atomics, ~9.6 us per launch), [P3D_SERVE_FLAG0 + 64 g + r] flag of member r
+// of group g
+#define P3D_SERVE_FLAG0 256
+#define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 32)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
@@ -100,10 +105,12 @@ struct ServeArgs {
   int L, K0, ND, nblk; // linear_size, input_size (<= 64), output_size (<= 64), residual blocks
   int bn, residual; float eps;
   float* act;          // [8][3][64 * L] packed activations per XCD group
-  float* part;         // [8][2][U][4 * NDT * 256] output partials per XCD group (step parity)
+  float* part;         // [groups][2][L/16][4 * NDT * 256] output partials per XCD group (step parity)
   unsigned* sync;      // P3D_SERVE_SYNC_WORDS, zeroed before every launch
   int* err;            // set to 1 when a bounded spin ran out
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
+  int split;           // k_serve6: groups per XCD (1..4)
+  const float* ec;     // k_serve6: epilogue constants [layer][L/16 tiles][bias 16 | inv 16 | shift 16] (k_serve_prep)
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 
@@ -114,6 +121,40 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_rsrc(const void* p) {
 // another CU of the group produced goes through this
 __device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
+}
+
+// Census (thread 0 of every workgroup): the XCD id read from the hardware, the workgroup's
+// rank within its XCD (one returning atomic on that XCD's counter), then a wait until the
+// eight counters sum to the grid (every workgroup resident, every count final).  sh[0] = XCD,
+// sh[1] = rank, sh[8 + x] = workgroups on XCD x, sh[2] = 1 if the wait timed out or an XCD
+// holds more than maxn workgroups (the flag barriers poll one lane per member).
+__device__ __forceinline__ void p3d_serve_census(const ServeArgs& p, int* sh, int maxn) {
+  if (threadIdx.x == 0) {
+    unsigned xr;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+    const int xcc = (int)(xr & 7u);
+    const unsigned rank = __hip_atomic_fetch_add(p.sync + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int bad = 0, spin = 0;
+    unsigned c[8];
+    while (true) {
+      unsigned tot = 0;
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        c[x] = __hip_atomic_load(p.sync + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tot += c[x];
+      }
+      if (tot >= gridDim.x) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
+    }
+    sh[0] = xcc; sh[1] = (int)rank;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) sh[8 + x] = (int)c[x];
+    if ((int)c[xcc] > maxn) bad = 1;
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[2] = bad;
+  }
+  __syncthreads();
 }
 
 // ---- register ring -------------------------------------------------------------------
@@ -418,28 +459,8 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
   const int rt = w >> 1, ct = w & 1;         // this wave's output tile of a unit
   const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
 
-  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
-  if (tid == 0) {
-    unsigned xr;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
-    const int xcc = (int)(xr & 7u);
-    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int bad = 0, spin = 0;
-    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
-    }
-    sh[0] = xcc; sh[1] = (int)rank;
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
-    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh[2] = bad;
-  }
-  __syncthreads();
+  // ---- census: XCD id, rank within the XCD, wait for every workgroup -----------------
+  p3d_serve_census(p, sh, 64);
   if (sh[2]) return;
   const int xcc = sh[0], r = sh[1], n = sh[8 + xcc];
   int ng = 0, gi = 0;
@@ -450,7 +471,7 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
     ng = p.max_groups;
     if (gi >= ng) gi = p.nb;   // this group takes no steps
   }
-  unsigned* flags = p.sync + 64 + 64 * xcc;
+  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * xcc;
   const int64_t slab = (int64_t)64 * L;
   float* act = p.act + (int64_t)xcc * 3 * slab;
   constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial
@@ -596,28 +617,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int L = p.L, ngL = L >> 4, U = L >> 5, ngK0 = p.K0 >> 4;
   const int q4 = 4 * (lane >> 4);
 
-  // ---- census: XCD id, rank within the XCD group, wait for every workgroup ---------
-  if (tid == 0) {
-    unsigned xr;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
-    const int xcc = (int)(xr & 7u);
-    const unsigned rank = __hip_atomic_fetch_add(p.sync + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(p.sync + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int bad = 0, spin = 0;
-    while (__hip_atomic_load(p.sync + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
-    }
-    sh[0] = xcc; sh[1] = (int)rank;
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-      sh[8 + x] = (int)__hip_atomic_load(p.sync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sh[8 + xcc] > 64) bad = 1;   // flag barrier: one polling lane per member
-    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh[2] = bad;
-  }
-  __syncthreads();
+  // ---- census: XCD id, rank within the XCD, wait for every workgroup -----------------
+  p3d_serve_census(p, sh, 64);
   if (sh[2]) return;
   const int xcc = sh[0], rx = sh[1], nx = sh[8 + xcc];
   const int half = rx % SPLIT;                          // group = (XCD, rank mod SPLIT)
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ng = p.max_groups;
     if (gi >= ng) gi = p.nb;   // this group takes no steps
   }
-  unsigned* flags = p.sync + 64 + 64 * gid;
+  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;
   const int64_t slab = (int64_t)64 * L;
   float* act = p.act + (int64_t)gid * 3 * slab;
   constexpr int PT = 4 * NDT * 256;          // floats of one unit's partial

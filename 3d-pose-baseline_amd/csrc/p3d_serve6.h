@@ -1,0 +1,499 @@
+// p3d_serve6.h -- k_serve6: the persistent XCD-local batch-64 evaluation sized for launches of
+// a few dozen steps (the driver's `bench.py --steps 20`).
+//
+// k_serve5 (p3d_serve.h) is built for throughput over long launches: two 16-CU groups per XCD,
+// each running its steps one after another.  With 20 steps per launch that leaves 4 of its 16
+// groups running a second step while the other 12 idle: the launch costs two steps of latency
+// (8 hidden phases, each ~20 us) for 1.25 steps of work.  The critical path of a launch of nb
+// steps is (rounds of steps) x (phases) x (column tiles per CU + fixed cost per phase), so
+// k_serve6 takes the groups-per-XCD S as a launch argument, chosen on the host for nb
+// (p3d.hip, serve6_split): at nb = 20, S = 3 groups of 11/11/10 CUs run all 20 steps at once,
+// each CU contracting <= 7 of a layer's 64 column tiles per phase -- 28 16x16 tiles of K = 1024
+// on the critical path and 4 phases, instead of 32 tiles and 8 phases.
+//
+// What differs from k_serve5 (everything else -- census by hardware XCD id, flag hand-offs in
+// the XCD's L2, sc1 reads of other CUs' data, 4-wave K-split contraction with a register ring,
+// epilogue constants in LDS, steps pipelined when a group has several -- is the same design):
+//   * work is dealt in 16-column tiles, not 32-column units: member r of a group of n owns the
+//     contiguous tiles [T r / n, T (r+1) / n) (T = L / 16), i.e. floor or ceil of T / n, and
+//     contracts them (all 4 row tiles) as one contraction of NCM tiles (a member with fewer
+//     computes a copy of its last tile and stores nothing for it; one with more loops);
+//   * the fused output layer writes one 64 x 48 partial per column tile, and a step's output is
+//     their sum in a fixed association (4 slices of T/4 tiles in order, then the slices in
+//     order) -- independent of n and S, so every launch shape gives the same bits.
+#pragma once
+#include "p3d_serve.h"
+
+#define P3D_SERVE6_RE 2            // output-reduction elements per lane (E4 / n <= 128)
+
+// Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
+// rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
+// [0] start, [1] census, [2] input layer, [3] first hand-off; per hidden phase ph at 8 ph:
+// [0] begin, [1] contraction, [2] K-combine, [3] epilogue, [4] hand-off; at 8 (NH + 1): [0]
+// the output reduction.  wall_clock64 (100 MHz).
+#ifdef P3D_TRACE
+#define P3D_S6_STAMP(row, k)                                                              \
+  do {                                                                                    \
+    if (tr6 && (row) && threadIdx.x == 0) {                                               \
+      tr6[(k)] = wall_clock64();                                                          \
+      tr6[64 + (k)] = __builtin_amdgcn_s_memtime();                                       \
+    }                                                                                     \
+  } while (0)
+#else
+#define P3D_S6_STAMP(row, k) do { } while (0)
+#endif
+
+// The serve launch's prologue kernel (in place of a memset of the sync words, so no extra
+// launch): zero the sync words and form the epilogue constants of every layer 0..2N and
+// column -- bias, inv = gamma / sqrt(var + eps), shift = beta - mean * inv, the arithmetic of
+// every other path -- laid out per 16-column tile as k_serve6 keeps them in LDS, so its
+// workgroups copy them with one round of loads instead of forming them (five dependent
+// operand loads per element) at the start of every launch.
+__global__ __launch_bounds__(256) void k_serve_prep(ServeArgs p, float* ecg) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < P3D_SERVE_SYNC_WORDS) p.sync[i] = 0u;
+  const int L = p.L, nl = 2 * p.nblk + 1;
+  if (i >= nl * L) return;
+  const int l = i / L, col = i % L, t = col >> 4, j = col & 15;
+  const ServeLayer& ly = p.ly[l];
+  float inv = 1.f, shift = 0.f;
+  if (p.bn) {
+    inv = (1.0f / sqrtf(ly.mvar[col] + p.eps)) * ly.gamma[col];
+    shift = ly.beta[col] - ly.mmean[col] * inv;
+  }
+  float* e = ecg + ((int64_t)l * (L >> 4) + t) * 48;
+  e[j] = ly.bias[col]; e[16 + j] = inv; e[32 + j] = shift;
+}
+
+// owner of column tile t when T tiles are dealt contiguously over n members
+__device__ __forceinline__ int p3d_tile_owner(int t, int n, int T) { return ((t + 1) * n - 1) / T; }
+
+template <int DEPTH, int NDT, int NCM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve6(ServeArgs p) {
+  constexpr int RE = P3D_SERVE6_RE;
+  constexpr int PT = 4 * NDT * 256;          // floats of one tile's output partial
+  constexpr int E4 = 4 * NDT * 64;           // float4 elements of a step's output
+  constexpr int DA = NCM >= 7 && DEPTH > 2 ? 2 : DEPTH;   // activation ring depth
+#ifndef P3D_S6_PD
+  constexpr int PD = NCM <= 4 ? 2 : 1;       // ring slots prefetched off-contraction
+#else
+  constexpr int PD = P3D_S6_PD;
+#endif
+  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NCM * 64];   // [slice][rt][tile][lane]
+  __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64 * RE];       // split output reduction
+  // epilogue constants of the member's first NCM tiles, per layer 0..2N: bias | inv | shift
+  __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * NCM * 48];
+  __shared__ int sh[20];
+  // wave-uniform values the compiler cannot prove uniform (the wave index, everything read
+  // from the census in LDS) go through readfirstlane: they end in scalar registers, and
+  // buffer loads with a scalar offset need no per-lane waterfall loop
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
+  const int q4 = 4 * (lane >> 4);
+  const int S = p.split;
+#ifdef P3D_TRACE
+  const unsigned long long t_start = wall_clock64();
+  unsigned long long* tr6 = nullptr;
+#endif
+
+  // ---- census: XCD id, rank within the XCD, wait for every workgroup ---------------------
+  p3d_serve_census(p, sh, (S < 1 || S > 4) ? -1 : 64 * S);
+  if (!sh[2]) {
+  const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
+  const int nx = __builtin_amdgcn_readfirstlane(sh[8 + xcc]);
+  const int half = rx % S, r = rx / S;
+  const int n = (nx + S - 1 - half) / S;
+  const int gid = xcc * S + half;
+  // groups in order of decreasing size (h-major): with fewer steps than groups the larger
+  // groups -- fewer tiles per member -- take them
+  int ng = 0, gi = 0;
+  for (int h = 0; h < S; ++h)
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int cnt = (__builtin_amdgcn_readfirstlane(sh[8 + x]) + S - 1 - h) / S;
+      if (cnt > 0) { if (x == xcc && h == half) gi = ng; ++ng; }
+    }
+  if (p.max_groups > 0 && ng > p.max_groups) {
+    ng = p.max_groups;
+    if (gi >= ng) gi = p.nb;
+  }
+  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;
+  const int64_t slab = (int64_t)64 * L;
+  float* act = p.act + (int64_t)gid * 3 * slab;
+  float* part = p.part + (int64_t)gid * 2 * T * PT;
+  const ServeLayer& li = p.ly[0];
+  const ServeLayer& lo = p.ly[2 * p.nblk + 1];
+  const bool wsq_any = li.wsq != nullptr;
+  const int NH = 2 * p.nblk;
+  unsigned nsync = 0;
+  bool broken = false;
+  const int gb = (ngL * w) >> 2, gcount = ngL >> 2;      // this wave's K slice (k-groups)
+  const int t_lo = (T * r) / n, t_hi = (T * (r + 1)) / n; // this member's column tiles
+  // this member's share of a step's output elements (split reduction: <= 64 RE per member)
+  const int es = (int)(((int64_t)E4 * r) / n), ecnt = (int)(((int64_t)E4 * (r + 1)) / n) - es;
+#ifdef P3D_TRACE
+  {
+    const int ncmax = (T + n - 1) / n;
+    const bool row1 = (t_hi - t_lo == ncmax) && (t_lo == 0 || (T * (r - 1)) / n + ncmax != t_lo);
+    if (r == 0 || row1) tr6 = g_p3d_trace + (gid * 2 + (r == 0 ? 0 : 1)) * 128;
+    if (tr6 && tid == 0) { tr6[0] = t_start; tr6[1] = wall_clock64(); }
+  }
+#endif
+  bool trs = true;                           // stamping this step (the group's first)
+  const bool split_red = t_lo < t_hi && ecnt <= 64 * RE;
+
+  auto in_issue = [&](int64_t rbase, int c0, f32x4 (&xa)[4], f32x4 (&wb)[NCM][4]) {
+    int64_t rowc = rbase + 16 * w + (lane & 15);
+    rowc = rowc < p.M ? rowc : p.M - 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g < ngK0) xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+    const int nck = min(NCM, t_hi - c0);
+#pragma unroll
+    for (int cc = 0; cc < NCM; ++cc) {
+      const int t = c0 + (cc < nck ? cc : nck - 1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (g < ngK0) wb[cc][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
+    }
+  };
+  // the group's first step's input-layer operands, requested before the epilogue constants
+  // are copied (their latencies overlap)
+  f32x4 xa0[4], wb0[NCM][4];
+  if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * 64, t_lo, xa0, wb0);
+  {   // epilogue constants of this member's first NCM tiles (k_serve_prep formed them)
+    const int nl = NH + 1, per = NCM * 12;   // float4s per layer
+#pragma unroll 4
+    for (int idx = tid; idx < nl * per; idx += 256) {
+      const int l = idx / per, rem = idx % per, cc = rem / 12, q = rem % 12;
+      const int t = min(t_lo + cc, T - 1);
+      *(f32x4*)(ec + (l * NCM + cc) * 48 + 4 * q) = *(const f32x4*)(p.ec + ((int64_t)l * T + t) * 48 + 4 * q);
+    }
+    __syncthreads();
+  }
+  // epilogue of tile t (chunk position cc) of layer l: z = acc / maxnorm + b, relu(z * inv + shift)
+  auto epi_t = [&](int l, int cc, int t, f32x4 acc) -> f32x4 {
+    if (t - t_lo >= NCM)   // beyond the first chunk (more tiles than NCM): operands from memory
+      return p3d_epi_apply(p3d_epi_load(p.ly[l], 16 * t + q4, p.bn, p.eps), acc, wsq_any, p.bn, p.eps);
+    const float* e = ec + (l * NCM + cc) * 48 + q4;
+    const f32x4 b4 = *(const f32x4*)e, inv4 = *(const f32x4*)(e + 16), sh4 = *(const f32x4*)(e + 32);
+    const float mx = wsq_any ? fmaxf(sqrtf(*p.ly[l].wsq), 1.0f) : 1.0f;
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float z = (wsq_any ? acc[k] / mx : acc[k]) + b4[k];
+      o[k] = fmaxf(p.bn ? z * inv4[k] + sh4[k] : z, 0.0f);
+    }
+    return o;
+  };
+
+  // Group barrier (as k_serve5): drain, publish this member's phase, then each wave waits for
+  // the members that produced its K slice (tiles [gb, gb + gcount)) -- or all members (full)
+  auto group_sync = [&](bool full) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++nsync;
+    if (tid == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int m0 = full ? 0 : p3d_tile_owner(gb, n, T);
+    const int cnt = full ? n : p3d_tile_owner(gb + gcount - 1, n, T) - m0 + 1;
+    if (!broken) {
+      int spin = 0;
+      while (true) {
+        const unsigned v = lane < cnt ? __hip_atomic_load(flags + m0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : nsync;
+        if (__all(v >= nsync)) break;
+        if (++spin > P3D_SERVE_SPIN) {
+          broken = true;
+          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  };
+
+  // input layer (K0 = input_size <= 64) of the member's tiles for the rows of the step at
+  // rbase, row tile w, into act buffer cbuf: the rows loaded once, then every tile's weight
+  // fragments requested before the first MFMA (one round of load latency, not one per tile)
+  auto in_compute = [&](int c0, const f32x4 (&xa)[4], const f32x4 (&wb)[NCM][4], int cbuf) {
+    const int nck = min(NCM, t_hi - c0);
+#pragma unroll
+    for (int cc = 0; cc < NCM; ++cc) {
+      if (cc >= nck) continue;
+      const int t = c0 + cc;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (g < ngK0)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[cc][g][e], xa[g][e], acc, 0, 0, 0);
+      const f32x4 y = epi_t(0, t - t_lo, t, acc);
+      *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + t) * 64 + lane) * 4) = y;
+    }
+  };
+  auto in_layer = [&](int64_t rbase, int cbuf, int cfrom) {
+    for (int c0 = cfrom; c0 < t_hi; c0 += NCM) {
+      f32x4 xa[4], wb[NCM][4];
+      in_issue(rbase, c0, xa, wb);
+      in_compute(c0, xa, wb, cbuf);
+    }
+  };
+
+  // output of the step at row0 from its T tile partials: member's elements [es, es + ecnt),
+  // wave w sums slice w (tiles [T w / 4, T (w+1) / 4)) in tile order into LDS; red_store adds
+  // the four slices in slice order (after the caller's __syncthreads)
+  auto red_slices = [&](const float* pb) {
+    const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(pb);
+    const int tb = (T * w) >> 2, te = (T * (w + 1)) >> 2;
+#pragma unroll
+    for (int j = 0; j < RE; ++j) {
+      const int el = lane + 64 * j;
+      f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (el < ecnt && tb < te) {
+        ss = p3d_ld_sc1(rp, (tb * E4 + es + el) * 16);
+#pragma unroll 4
+        for (int t = tb + 1; t < te; ++t) ss += p3d_ld_sc1(rp, (t * E4 + es + el) * 16);
+      }
+      rsum[w * 64 * RE + el] = ss;
+    }
+  };
+  // the same sums with every partial requested before the first add (16 tiles per slice in
+  // flight: the launch's last reduction, nothing else is live then)
+  auto red_slices_all = [&](const float* pb) {
+    const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(pb);
+    const int tb = (T * w) >> 2, te = (T * (w + 1)) >> 2;
+#pragma unroll
+    for (int j = 0; j < RE; ++j) {
+      const int el = lane + 64 * j;
+      f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (el < ecnt && tb < te) {
+        for (int t0 = tb; t0 < te; t0 += 16) {
+          f32x4 v[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (t0 + k < te) v[k] = p3d_ld_sc1(rp, ((t0 + k) * E4 + es + el) * 16);
+          if (t0 == tb) ss = v[0];
+          else ss += v[0];
+#pragma unroll
+          for (int k = 1; k < 16; ++k)
+            if (t0 + k < te) ss += v[k];
+        }
+      }
+      rsum[w * 64 * RE + el] = ss;
+    }
+  };
+  auto red_store = [&](int64_t prow0) {      // after a __syncthreads
+    if (tid < ecnt) {
+      f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 * RE + tid];
+      p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prow0);
+    }
+  };
+  // non-split form (large T or small groups): same association, thread per element
+  auto red_plain = [&](const float* pb, int64_t prow0) {
+    const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
+    for (int e4 = es + tid; e4 < es + ecnt; e4 += 256) {
+      f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < 4; ++sl) {
+        const int tb = (T * sl) >> 2, te = (T * (sl + 1)) >> 2;
+        if (tb == te) continue;
+        f32x4 ss = p3d_ld_sc1(rs, (tb * E4 + e4) * 16);
+        for (int t = tb + 1; t < te; ++t) ss += p3d_ld_sc1(rs, (t * E4 + e4) * 16);
+        sum += ss;
+      }
+      p3d_serve_store_out<NDT>(p, lo, sum, e4, prow0);
+    }
+  };
+
+  f32x4 rbp[PD][NCM];                        // the next ring's first weight fragments
+  auto b_prefetch = [&](int layer, int c0) {   // c0 < t_hi
+    const int nck = min(NCM, t_hi - c0);
+#pragma unroll
+    for (int cc = 0; cc < NCM; ++cc) {
+      const int t = c0 + (cc < nck ? cc : nck - 1);
+      const f32x4* pbn = (const f32x4*)p.ly[layer].Wf + ((int64_t)t * ngL + gb) * 64 + lane;
+#pragma unroll
+      for (int d = 0; d < PD; ++d) rbp[d][cc] = pbn[d * 64];
+    }
+  };
+
+  int jl = 0, c0b = 0;
+  int64_t prev_row0 = -1;
+  if (gi < p.nb) {                           // the group's first step: its input layer alone
+    if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, 0);
+    in_layer((int64_t)gi * 64, 0, t_lo + NCM);
+    P3D_S6_STAMP(trs, 2);
+    if (t_lo < t_hi) b_prefetch(1, t_lo);
+    group_sync(false);
+    P3D_S6_STAMP(trs, 3);
+  }
+  for (int b = gi; b < p.nb; b += ng, ++jl) {
+    const int64_t row0 = (int64_t)b * 64;
+    const bool has_next = b + ng < p.nb;
+    const int c0n = (c0b + 2 * p.nblk) % 3;  // buffer the next step's input layer writes
+    int cur = c0b;
+    float* pdst = part + (int64_t)(jl & 1) * T * PT;
+    const float* prev_part = part + (int64_t)((jl - 1) & 1) * T * PT;
+    for (int ph = 1; ph <= NH; ++ph) {
+      P3D_S6_STAMP(trs, 8 * ph);
+      const bool lastp = (ph == NH);
+      const bool red_here = (ph == 1 && prev_row0 >= 0);
+      if (red_here && !split_red) red_plain(prev_part, prev_row0);
+      const ServeLayer& ly = p.ly[ph];
+      const bool second = ((ph - 1) & 1) == 1;
+      const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
+      const float* A = act + (second ? t1 : cur) * slab;
+      float* Y = act + (second ? t2 : t1) * slab;
+      const float* res = (second && p.residual) ? act + cur * slab : nullptr;
+      const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
+      const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
+      for (int c0 = t_lo; c0 < t_hi; c0 += NCM) {
+        const bool first_c = (c0 == t_lo);
+        const int nck = min(NCM, t_hi - c0);
+        // weight fragments through a buffer resource: one lane offset, tile / k-group offsets
+        // scalar (tile cc's fragments at (c0 + cc) ngL + gb + g; a copy of the last past nck)
+        const __amdgpu_buffer_rsrc_t rw = p3d_rsrc(ly.Wf);
+        const int voff = lane * 16;
+        int toff[NCM];
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc) toff[cc] = ((c0 + (cc < nck ? cc : nck - 1)) * ngL + gb) * 1024;
+        auto ldb = [&](int cc, int g) -> f32x4 {
+          return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, voff, toff[cc] + g * 1024, 0));
+        };
+        // register ring: weight fragments DEPTH k-groups ahead, activations DA ahead (the
+        // weights stream from MALL/HBM, the activations are L2 hits; the wide forms cannot hold
+        // both DEPTH deep: 4 x 11 fragments spilled 77 registers at NCM = 7)
+        f32x4 ra_[DA][4], rb_[DEPTH][NCM];
+        // the first PD weight slots were requested off the previous contraction (b_prefetch
+        // runs before every contraction); a compile-time split keeps the number of loads in
+        // flight static, so the compiler's vmcnt waits stay exact
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+          if (d < DA)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+#pragma unroll
+          for (int cc = 0; cc < NCM; ++cc) rb_[d][cc] = d < PD ? rbp[d < PD ? d : 0][cc] : ldb(cc, d);
+        }
+        f32x4 acc[NCM][4];
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[cc][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto mfmas = [&](int d) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d % DA][t][e], acc[cc][t], 0, 0, 0);
+        };
+        for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
+#pragma unroll
+          for (int d = 0; d < DEPTH; ++d) {
+            mfmas(d);
+            const int ga = g0 + d + DA, gn = g0 + DEPTH + d;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
+#pragma unroll
+            for (int cc = 0; cc < NCM; ++cc) rb_[d][cc] = ldb(cc, gn);
+            __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {        // the last DEPTH k-groups
+          mfmas(d);
+          if (d + DA < DEPTH) {
+            const int ga = gcount - DEPTH + d + DA;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        // ---- off-contraction loads, their latency under the combine and epilogue ----------
+        __builtin_amdgcn_sched_barrier(0);
+        P3D_S6_STAMP(trs && first_c, 8 * ph + 1);
+        // the epilogue's operands first (vmcnt waits are in order: the epilogue then waits for
+        // them only, not for the next ring's weights behind them)
+        const bool red_now = red_here && split_red && first_c;
+        // requested unconditionally (the residual operands from A where there is no residual,
+        // W4 in every phase): conditional loads would make the compiler's vmcnt waits
+        // conservative, i.e. wait for the next ring's weights behind them as well
+        f32x4 rv[NCM], wo[NCM][NDT];
+        const __amdgpu_buffer_rsrc_t rr = p3d_rsrc(res ? res : A);
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc) {
+          const int t = c0 + (cc < nck ? cc : nck - 1);
+          rv[cc] = p3d_ld_sc1(rr, (int)(((int64_t)(w * ngL + t) * 64 + lane) * 16));
+          p3d_wo_load<NDT>(lo, t, ngL, wo[cc]);
+        }
+        // the next contraction's first weight slots: this member's next chunk, the next
+        // layer, or the next step's first layer (requested even after a group's last step:
+        // a fixed number of loads keeps the vmcnt waits exact)
+        {
+          const bool more = c0 + NCM < t_hi;
+          b_prefetch(more ? ph : (!lastp ? ph + 1 : 1), more ? c0 + NCM : t_lo);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- K-slice combine (LDS), epilogue ----------------------------------------------
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) red[((w * 4 + t) * NCM + cc) * 64 + lane] = acc[cc][t];
+        if (red_now) red_slices(prev_part);   // the previous step's output (acc is dead here)
+        __syncthreads();
+        P3D_S6_STAMP(trs && first_c, 8 * ph + 2);
+        if (red_now) red_store(prev_row0);
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc) {
+          if (cc >= nck) continue;
+          const int t = c0 + cc;
+          f32x4 sacc = red[((0 * 4 + w) * NCM + cc) * 64 + lane];   // slice 0, tile (w, cc)
+#pragma unroll
+          for (int k = 1; k < 4; ++k) sacc += red[((k * 4 + w) * NCM + cc) * 64 + lane];
+          f32x4 yv = epi_t(ph, t - t_lo, t, sacc);
+          if (res) yv += rv[cc];
+          if (lastp) {                         // fused output layer: this tile's 64 x 48 partial
+#pragma unroll
+            for (int o = 0; o < NDT; ++o) {
+              f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[cc][o][e], pacc, 0, 0, 0);
+              *(f32x4*)(pdst + (int64_t)t * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
+            }
+          } else {
+            *(f32x4*)(Y + ((int64_t)(w * ngL + t) * 64 + lane) * 4) = yv;
+          }
+        }
+        // red / rsum are rewritten by this member's next contraction of the phase
+        if (c0 + NCM < t_hi) __syncthreads();
+      }
+      // the next step's input layer (it depends on nothing of this step) in the last phase
+      if (lastp && has_next) in_layer(row0 + (int64_t)ng * 64, c0n, t_lo);
+      P3D_S6_STAMP(trs, 8 * ph + 3);
+      if (second) cur = t2;
+      // after a step's last phase the output reduction reads every tile's partial: the split
+      // form reads exactly the wave's producers' (its K slice), the plain form all of them
+      group_sync(lastp && (!has_next || !split_red));
+      P3D_S6_STAMP(trs, 8 * ph + 4);
+    }
+    trs = false;
+    prev_row0 = row0;
+    c0b = c0n;
+  }
+  if (prev_row0 >= 0) {                      // the group's last step's output
+    const float* pb = part + (int64_t)((jl - 1) & 1) * T * PT;
+    if (split_red) {
+      red_slices_all(pb);
+      __syncthreads();
+      red_store(prev_row0);
+    } else {
+      red_plain(pb, prev_row0);
+    }
+#ifdef P3D_TRACE
+    if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
+#endif
+  }
+  }
+}

@@ -296,6 +296,19 @@ def bench_serve(args, rank, world):
     dt = max_over_ranks(time.perf_counter() - t0, world)
     model.serve_check()
     value = world * args.steps * BATCH / dt
+    # where the wall time of a launch goes (diagnostic, untimed): host enqueue of one launch,
+    # one launch + synchronize round trip, synchronize of an idle device (medians)
+    import torch
+    def med(fn, n=30):
+        ts = []
+        for _ in range(n):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t)
+        return round(1e6 * sorted(ts)[len(ts) // 2], 2)
+    host = {"enqueue_us": med(lambda: run(1)), "launch_sync_us": med(lambda: (run(1), torch.cuda.synchronize())),
+            "idle_sync_us": med(torch.cuda.synchronize)}
     # dominant (only) kernel, timed live: R launches, each carrying a start/stop event pair
     # attached to its dispatch (hipExtLaunchKernel), the interval rocprofv3 reports
     prof = profile_kernels(model, lambda: run(R))
@@ -310,7 +323,7 @@ def bench_serve(args, rank, world):
             "kernel": kname + " (persistent: %d batch-64 steps per launch, whole network per XCD, fp32 MFMA 16x16x4)" % C,
             "flop_per_launch": int(flop), "steps_per_launch": C, "warmup_launches": wl, "avg_us": round(avg_us, 3),
             "launches_timed": cnt,
-            "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}}
+            "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}, "host_us": host}
     model.close()
     return value, dt, roof
 

@@ -140,3 +140,107 @@ def test_serve_knob_variants_vs_oracle(monkeypatch, split, upm, depth, L, N):
     ro, _ = ref_mlp.forward(st, x[idx], False, 1.0, 0, 0, 0)
     close(y.cpu().numpy()[idx], ro)
     m.close()
+
+
+def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1):
+    if split is not None:
+        monkeypatch.setenv("P3D_SERVE6_SPLIT", str(split))
+    if mode is not None:
+        monkeypatch.setenv("P3D_SERVE6", str(mode))
+    st, m = make(cfg, seed=seed)
+    monkeypatch.delenv("P3D_SERVE6_SPLIT", raising=False)
+    monkeypatch.delenv("P3D_SERVE6", raising=False)
+    return st, m
+
+
+def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
+    """k_serve6 (launches of <= 32 steps; the driver's 20-step headline): 1, 2, 3 or 4 groups
+    per XCD (16-column tiles dealt contiguously, 7 tiles per CU at 3 groups) give the same bits --
+    the association of every sum is fixed by the tile, not by the group shape -- and the
+    oracle's outputs; the auto choice for 20 steps is the 3-group form."""
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    B = 64 * 20
+    x = np.random.default_rng(620).standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    outs = {}
+    for split in (None, 1, 2, 3, 4):
+        st, m = _serve6_model(monkeypatch, cfg, split)
+        y = m.serve_device(xd)
+        torch.cuda.synchronize()
+        m.serve_check()
+        name = _p3d.ctypes.create_string_buffer(128)
+        _p3d.check(_p3d.lib().p3d_kernel_name(m._h, 3, name, 128), "p3d_kernel_name")
+        assert name.value.decode().startswith("k_serve6<"), name.value
+        outs[split] = (y, name.value.decode())
+        m.close()
+    assert outs[None][1] == "k_serve6<2, 3, 7>", outs[None][1]     # nb = 20 -> 3 groups per XCD
+    for split in (1, 2, 3, 4):
+        assert torch.equal(outs[split][0], outs[None][0]), split
+    ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+    close(outs[None][0].cpu().numpy(), ro)
+
+
+@pytest.mark.parametrize("B", [1, 13, 64, 64 * 5 + 7, 64 * 8, 64 * 16, 64 * 24 + 1, 64 * 32])
+def test_serve6_launch_sizes_vs_oracle(B):
+    """Every launch size k_serve6 takes (<= 32 steps; the split chosen per launch), ragged
+    tails, against the oracle; and equal bits whatever the launch size (same rows)."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    x = np.random.default_rng(B).standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    y = m.serve_device(xd)
+    m.serve_check()
+    ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+    close(y.cpu().numpy(), ro)
+    if B >= 64:   # the first step alone as its own launch: same bits
+        assert torch.equal(m.serve_device(xd[:64]), y[:64])
+    m.close()
+
+
+@pytest.mark.parametrize("L,N,residual,batch_norm,max_norm,p14", [
+    (256, 1, True, True, False, False),      # cfg1: 16 tiles, idle members at 1-2 groups per XCD
+    (512, 3, True, True, True, False),       # max-norm, three blocks
+    (1024, 2, False, False, False, False),   # no BN, no residual
+    (1024, 2, True, True, False, True),      # --predict_14
+    (2048, 1, True, True, False, False),     # 128 tiles: 13 per CU at 3 groups -> two contractions
+])
+@pytest.mark.parametrize("split", [None, 3])
+def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split):
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
+                      predict_14=p14)
+    st, m = _serve6_model(monkeypatch, cfg, split)
+    B = 64 * 20 + 5
+    x = np.random.default_rng(L + N).standard_normal((B, 32)).astype(np.float32)
+    y = m.serve_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    m.serve_check()
+    ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
+    close(y, ro, atol=5e-5, rtol=5e-5)
+    m.close()
+
+
+@pytest.mark.parametrize("split", [1, 2, 3])
+def test_serve6_many_steps_per_group(monkeypatch, split):
+    """k_serve6 forced on a long launch (P3D_SERVE6=2): every group runs many steps, so the
+    next step's input layer rides in the last phase and each step's output is reduced in the
+    next step's first phase (split over the members); every row vs the oracle / k_serve5."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    B = 64 * 300 + 9
+    x = np.random.default_rng(77 + split).standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    st, m6 = _serve6_model(monkeypatch, cfg, split, mode=2)
+    y6 = m6.serve_device(xd)
+    torch.cuda.synchronize()
+    m6.serve_check()
+    _, m5 = _serve6_model(monkeypatch, cfg, mode=0)
+    y5 = m5.serve_device(xd)
+    torch.cuda.synchronize()
+    m5.serve_check()
+    close(y6.cpu().numpy(), y5.cpu().numpy(), atol=5e-5, rtol=5e-5)
+    idx = np.r_[0:64, np.random.default_rng(2).choice(B, 448, replace=False), B - 9:B]
+    ro, _ = ref_mlp.forward(st, x[idx], False, 1.0, 0, 0, 0)
+    close(y6.cpu().numpy()[idx], ro)
+    # the same rows as a 20-step launch: same bits
+    assert torch.equal(m6.serve_device(xd[:64 * 20]), y6[:64 * 20])
+    m6.close()
+    m5.close()

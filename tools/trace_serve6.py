@@ -1,0 +1,68 @@
+"""Dev tool: timeline of one k_serve6 launch from a -DP3D_TRACE build.
+
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -munsafe-fp-atomics -DP3D_TRACE \\
+        -o 3d-pose-baseline_amd/libp3d_trace.so 3d-pose-baseline_amd/csrc/p3d.hip
+    P3D_LIB=$PWD/3d-pose-baseline_amd/libp3d_trace.so python tools/trace_serve6.py [steps] [reps]
+
+For every XCD group of the last launch (its first step): rank-0 member and the first member
+holding the most column tiles; times in us from the earliest workgroup start (wall_clock64,
+100 MHz).  Columns per hidden phase: contraction, K-combine, epilogue, hand-off wait.
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _p3d  # noqa: E402
+import linear_model  # noqa: E402
+
+
+def main():
+    nb = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_probe", seed=3, max_batch=64)
+    x = torch.randn((64 * nb, 32), device="cuda")
+    for _ in range(reps):
+        m.serve_device(x)
+    torch.cuda.synchronize()
+    m.serve_check()
+    lib = _p3d.lib()
+    lib.p3d_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = np.zeros(4096 * 8, np.uint64)
+    assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
+    t = buf[:64 * 128].astype(np.int64).reshape(32, 2, 128)
+    NH = 4
+    live = [(g, r) for g in range(32) for r in range(2) if t[g, r, 0] and t[g, r, 8 * (NH + 1)]]
+    t0 = min(t[g, r, 0] for g, r in live)
+    us = lambda v: round((v - t0) / 100.0, 2)   # noqa: E731
+    out = []
+    for g, r in live:
+        row = t[g, r]
+        if row[8 * (NH + 1)] < row[0]:          # stale (a group idle in the last launch)
+            continue
+        ph = []
+        for p in range(1, NH + 1):
+            b, c, k, e, h = (row[8 * p + i] for i in range(5))
+            ph.append([round((c - b) / 100, 2), round((k - c) / 100, 2), round((e - k) / 100, 2),
+                       round((h - e) / 100, 2)])
+        # core clock over the contractions: s_memtime cycles / wall_clock64 (100 MHz) ticks
+        cyc = sum(row[64 + 8 * p + 1] - row[64 + 8 * p] for p in range(1, NH + 1))
+        wall = sum(row[8 * p + 1] - row[8 * p] for p in range(1, NH + 1))
+        out.append({"group": g, "row": r, "clock_ghz": round(cyc / max(wall, 1) / 10.0, 3), "start": us(row[0]), "census": us(row[1]), "input": us(row[2]),
+                    "handoff0": us(row[3]), "end_phase": [us(row[8 * p + 4]) for p in range(1, NH + 1)],
+                    "reduce_end": us(row[8 * (NH + 1)]), "phases_us": ph})
+    out.sort(key=lambda d: d["reduce_end"])
+    for d in out:
+        print(json.dumps(d))
+    print("launch end (latest reduce): %.2f us" % max(d["reduce_end"] for d in out))
+
+
+if __name__ == "__main__":
+    main()
