@@ -1992,15 +1992,25 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
 // (hand-off, ring fill, K-combine, epilogue) ~4 us, a column tile of K = 1024 ~3.9 us
 // (round-1 phase traces).  nb = 20 -> S = 3 (all steps at once, <= 7 tiles per
 // CU); nb <= 8 -> S = 1; nb = 16 -> S = 2.
+static int serve6_ncm(const p3d_model* m, int S, int T);
+// tiles a member of the smallest group holds, and whether the form built for it covers them
+// (a member keeps the epilogue constants of at most ECT tiles in LDS, p3d_serve6.h)
+static bool serve6_fits(const p3d_model* m, int S, int T) {
+  const int nmin = std::max(1, m->serve_grid / 8) / S;
+  if (nmin < 1) return false;
+  const int need = (T + nmin - 1) / nmin, ncm = serve6_ncm(m, S, T);
+  return need <= (ncm >= 7 ? ncm : 2 * ncm);
+}
+
 static int serve6_split_for(const p3d_model* m, int64_t nb, int T) {
-  if (m->serve6_split >= 1 && m->serve6_split <= 4) return m->serve6_split;
+  if (m->serve6_split >= 1 && m->serve6_split <= 4) return serve6_fits(m, m->serve6_split, T) ? m->serve6_split : 0;
   const int cx = std::max(1, m->serve_grid / 8);
   const double cfix = 4.0, ctile = 3.9 * T / 64.0;
-  int best = 1;
+  int best = 0;
   double bt = 1e30;
   for (int S = 1; S <= 4; ++S) {
     const int nmin = cx / S;
-    if (nmin < 1) break;
+    if (nmin < 1 || !serve6_fits(m, S, T)) continue;
     const double rounds = (double)((nb + 8 * S - 1) / (8 * S));
     const double t = rounds * (cfix + ctile * ((T + nmin - 1) / nmin));
     if (t < bt - 1e-9) { bt = t; best = S; }
@@ -2084,8 +2094,11 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     }
     s.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
   }
-  const bool use6 = m->serve6 && c.num_layers > 0 && NDT == 3 &&
-                    (m->serve6 == 2 || a.nb <= (int64_t)m->serve6_max_nb);
+  bool use6 = m->serve6 && c.num_layers > 0 && NDT == 3 && (m->serve6 == 2 || a.nb <= (int64_t)m->serve6_max_nb);
+  if (use6) {
+    a.split = serve6_split_for(m, a.nb, L / 16);
+    use6 = a.split > 0;                      // no form covers this width: k_serve5
+  }
   if (use6) {
     // one prologue launch: sync words zeroed + epilogue constants formed (k_serve_prep)
     a.ec = m->serve_ec;
@@ -2096,7 +2109,6 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   }
   if (use6) {
     const int T = L / 16;
-    a.split = serve6_split_for(m, a.nb, T);
     const int ncm = serve6_ncm(m, a.split, T);
     const int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
     m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ">";
@@ -2125,7 +2137,8 @@ extern "C" int p3d_serve_check(p3d_model* m) {
     // reported once: the word and the sync words are cleared, so later launches are judged
     // on their own (every launch re-zeroes the sync words before it starts anyway)
     hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned));
-    return fail(P3D_ERR_HIP, "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
+    return fail(P3D_ERR_HIP, v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
+                                    : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
   }
   return P3D_OK;
 }

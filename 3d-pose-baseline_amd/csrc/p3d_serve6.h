@@ -63,6 +63,8 @@ __global__ __launch_bounds__(256) void k_serve_prep(ServeArgs p, float* ecg) {
   }
   float* e = ecg + ((int64_t)l * (L >> 4) + t) * 48;
   e[j] = ly.bias[col]; e[16 + j] = inv; e[32 + j] = shift;
+  if (col == 0)   // the layer's max-norm divisor max(||W||, 1) (1 without --max_norm)
+    ecg[(int64_t)nl * (L >> 4) * 48 + l] = ly.wsq ? fmaxf(sqrtf(*ly.wsq), 1.0f) : 1.0f;
 }
 
 // owner of column tile t when T tiles are dealt contiguously over n members
@@ -81,8 +83,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NCM * 64];   // [slice][rt][tile][lane]
   __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64 * RE];       // split output reduction
-  // epilogue constants of the member's first NCM tiles, per layer 0..2N: bias | inv | shift
-  __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * NCM * 48];
+  // epilogue constants of the member's tiles (up to ECT of them), per layer 0..2N:
+  // bias | inv | shift, and each layer's max-norm divisor.  Every epilogue reads them from
+  // LDS: no global load on a branch of the epilogue, so the compiler's vmcnt waits there stay
+  // exact (a load on a not-taken branch had made them wait for every load in flight).
+  constexpr int ECT = NCM >= 7 ? NCM : 2 * NCM;
+  __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * ECT * 48];
+  __shared__ float ecm[P3D_SERVE_MAXL];
   __shared__ int sh[20];
   // wave-uniform values the compiler cannot prove uniform (the wave index, everything read
   // from the census in LDS) go through readfirstlane: they end in scalar registers, and
@@ -116,6 +123,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (p.max_groups > 0 && ng > p.max_groups) {
     ng = p.max_groups;
     if (gi >= ng) gi = p.nb;
+  }
+  if ((T + n - 1) / n > ECT) {               // a placement the host did not size this form for:
+    if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gi = p.nb;                               // the whole group reports instead of computing
   }
   unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;
   const int64_t slab = (int64_t)64 * L;
@@ -161,30 +172,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // are copied (their latencies overlap)
   f32x4 xa0[4], wb0[NCM][4];
   if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * 64, t_lo, xa0, wb0);
-  {   // epilogue constants of this member's first NCM tiles (k_serve_prep formed them)
-    const int nl = NH + 1, per = NCM * 12;   // float4s per layer
+  {   // epilogue constants of this member's tiles (k_serve_prep formed them)
+    const int nl = NH + 1, per = ECT * 12;   // float4s per layer
 #pragma unroll 4
     for (int idx = tid; idx < nl * per; idx += 256) {
       const int l = idx / per, rem = idx % per, cc = rem / 12, q = rem % 12;
       const int t = min(t_lo + cc, T - 1);
-      *(f32x4*)(ec + (l * NCM + cc) * 48 + 4 * q) = *(const f32x4*)(p.ec + ((int64_t)l * T + t) * 48 + 4 * q);
+      *(f32x4*)(ec + (l * ECT + cc) * 48 + 4 * q) = *(const f32x4*)(p.ec + ((int64_t)l * T + t) * 48 + 4 * q);
     }
+    if (tid < nl) ecm[tid] = p.ec[(int64_t)nl * T * 48 + tid];
     __syncthreads();
   }
   // epilogue of tile t (chunk position cc) of layer l: z = acc / maxnorm + b, relu(z * inv + shift)
-  auto epi_t = [&](int l, int cc, int t, f32x4 acc) -> f32x4 {
-    if (t - t_lo >= NCM)   // beyond the first chunk (more tiles than NCM): operands from memory
-      return p3d_epi_apply(p3d_epi_load(p.ly[l], 16 * t + q4, p.bn, p.eps), acc, wsq_any, p.bn, p.eps);
-    const float* e = ec + (l * NCM + cc) * 48 + q4;
+  // acc already divided by the max-norm divisor (maxnorm_div, a uniform branch of its own:
+  // a per-element select made every epilogue run the division sequence)
+  auto epi_t = [&](int l, int cs, f32x4 acc) -> f32x4 {   // cs = tile - t_lo < ECT
+    const float* e = ec + (l * ECT + cs) * 48 + q4;
     const f32x4 b4 = *(const f32x4*)e, inv4 = *(const f32x4*)(e + 16), sh4 = *(const f32x4*)(e + 32);
-    const float mx = wsq_any ? fmaxf(sqrtf(*p.ly[l].wsq), 1.0f) : 1.0f;
     f32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float z = (wsq_any ? acc[k] / mx : acc[k]) + b4[k];
+      const float z = acc[k] + b4[k];
       o[k] = fmaxf(p.bn ? z * inv4[k] + sh4[k] : z, 0.0f);
     }
     return o;
+  };
+  auto maxnorm_div = [&](int l, f32x4& acc) {
+    const float mx = ecm[l];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = acc[k] / mx;
   };
 
   // Group barrier (as k_serve5): drain, publish this member's phase, then each wave waits for
@@ -226,7 +242,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (g < ngK0)
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[cc][g][e], xa[g][e], acc, 0, 0, 0);
-      const f32x4 y = epi_t(0, t - t_lo, t, acc);
+      if (wsq_any) maxnorm_div(0, acc);
+      const f32x4 y = epi_t(0, t - t_lo, acc);
       *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + t) * 64 + lane) * 4) = y;
     }
   };
@@ -241,21 +258,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // output of the step at row0 from its T tile partials: member's elements [es, es + ecnt),
   // wave w sums slice w (tiles [T w / 4, T (w+1) / 4)) in tile order into LDS; red_store adds
   // the four slices in slice order (after the caller's __syncthreads)
-  auto red_slices = [&](const float* pb) {
-    const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(pb);
-    const int tb = (T * w) >> 2, te = (T * (w + 1)) >> 2;
-#pragma unroll
-    for (int j = 0; j < RE; ++j) {
-      const int el = lane + 64 * j;
-      f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (el < ecnt && tb < te) {
-        ss = p3d_ld_sc1(rp, (tb * E4 + es + el) * 16);
-#pragma unroll 4
-        for (int t = tb + 1; t < te; ++t) ss += p3d_ld_sc1(rp, (t * E4 + es + el) * 16);
-      }
-      rsum[w * 64 * RE + el] = ss;
-    }
-  };
   // the same sums with every partial requested before the first add (16 tiles per slice in
   // flight: the launch's last reduction, nothing else is live then)
   auto red_slices_all = [&](const float* pb) {
@@ -338,7 +340,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       P3D_S6_STAMP(trs, 8 * ph);
       const bool lastp = (ph == NH);
       const bool red_here = (ph == 1 && prev_row0 >= 0);
+      // the previous step's output (groups running several steps): before the contraction,
+      // not inside its epilogue -- loads on a branch there made the compiler's waits in the
+      // epilogue wait for every load in flight
       if (red_here && !split_red) red_plain(prev_part, prev_row0);
+      if (red_here && split_red) {
+        red_slices_all(prev_part);
+        __syncthreads();
+        red_store(prev_row0);
+        __syncthreads();
+      }
       const ServeLayer& ly = p.ly[ph];
       const bool second = ((ph - 1) & 1) == 1;
       const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
@@ -416,7 +427,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         P3D_S6_STAMP(trs && first_c, 8 * ph + 1);
         // the epilogue's operands first (vmcnt waits are in order: the epilogue then waits for
         // them only, not for the next ring's weights behind them)
-        const bool red_now = red_here && split_red && first_c;
         // requested unconditionally (the residual operands from A where there is no residual,
         // W4 in every phase): conditional loads would make the compiler's vmcnt waits
         // conservative, i.e. wait for the next ring's weights behind them as well
@@ -441,18 +451,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int cc = 0; cc < NCM; ++cc)
 #pragma unroll
           for (int t = 0; t < 4; ++t) red[((w * 4 + t) * NCM + cc) * 64 + lane] = acc[cc][t];
-        if (red_now) red_slices(prev_part);   // the previous step's output (acc is dead here)
         __syncthreads();
         P3D_S6_STAMP(trs && first_c, 8 * ph + 2);
-        if (red_now) red_store(prev_row0);
+        f32x4 sacc[NCM];                       // K slices summed in slice order
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc) {
+          sacc[cc] = red[((0 * 4 + w) * NCM + cc) * 64 + lane];   // slice 0, tile (w, cc)
+#pragma unroll
+          for (int k = 1; k < 4; ++k) sacc[cc] += red[((k * 4 + w) * NCM + cc) * 64 + lane];
+        }
+        if (wsq_any)
+#pragma unroll
+          for (int cc = 0; cc < NCM; ++cc) maxnorm_div(ph, sacc[cc]);
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc) {
           if (cc >= nck) continue;
           const int t = c0 + cc;
-          f32x4 sacc = red[((0 * 4 + w) * NCM + cc) * 64 + lane];   // slice 0, tile (w, cc)
-#pragma unroll
-          for (int k = 1; k < 4; ++k) sacc += red[((k * 4 + w) * NCM + cc) * 64 + lane];
-          f32x4 yv = epi_t(ph, t - t_lo, t, sacc);
+          f32x4 yv = epi_t(ph, t - t_lo, sacc[cc]);
           if (res) yv += rv[cc];
           if (lastp) {                         // fused output layer: this tile's 64 x 48 partial
 #pragma unroll
