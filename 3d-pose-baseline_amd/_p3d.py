@@ -149,8 +149,12 @@ def ptr(t) -> int:
 
 def stream_handle(stream=None) -> int:
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+    if stream is None:
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)   # no Stream object built
+        if raw is not None:
+            return int(raw(torch.cuda.current_device()))
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
 
 
 __all__ = ["P3DCfg", "P3DError", "lib", "check", "device_view", "ptr", "stream_handle",

@@ -1226,7 +1226,8 @@ struct p3d_model {
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
-  float* serve_ec = nullptr;   // k_serve6 epilogue constants (k_serve_prep, every launch)
+  unsigned serve_epoch = 0;     // k_serve6 launches so far (sync-word bank = epoch & 1)
+  bool serve_banks_clean = true;   // both banks zero (false after a k_serve5 launch used bank 0)
   unsigned* serve_sync = nullptr;
   int* serve_err = nullptr;
   int serve_grid = 0;
@@ -1290,7 +1291,6 @@ void free_all(p3d_model* m) {
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
-  if (m->serve_ec) (void)hipFree(m->serve_ec);
 }
 }  // namespace
 
@@ -2069,13 +2069,13 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     if ((e = hipMemset(m->serve_buf, 0, nbuf * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    if ((e = hipMalloc(&m->serve_sync, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+    // [bank 0 | bank 1 | error word]: k_serve5 uses bank 0 (zeroed before each launch),
+    // k_serve6 alternates the banks (p3d_serve6.h)
+    if ((e = hipMalloc(&m->serve_sync, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    if ((e = hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+    if ((e = hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    m->serve_err = (int*)(m->serve_sync + P3D_SERVE_SYNC_WORDS);
-    if ((e = hipMalloc(&m->serve_ec, (size_t)P3D_SERVE_MAXL * L * 3 * sizeof(float))) != hipSuccess)
-      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    m->serve_err = (int*)(m->serve_sync + 2 * P3D_SERVE_SYNC_WORDS);
   }
   ServeArgs a{};
   a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);
@@ -2100,12 +2100,20 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     use6 = a.split > 0;                      // no form covers this width: k_serve5
   }
   if (use6) {
-    // one prologue launch: sync words zeroed + epilogue constants formed (k_serve_prep)
-    a.ec = m->serve_ec;
-    const int nwork = std::max(P3D_SERVE_SYNC_WORDS, (2 * c.num_layers + 1) * L);
-    hipLaunchKernelGGL(k_serve_prep, dim3((nwork + 255) / 256), dim3(256), 0, st, a, m->serve_ec);
-  } else if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess) {
-    return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    // no memset in front: this launch's bank was zeroed by the previous k_serve6 launch (or at
+    // allocation); after a k_serve5 launch (bank 0) both banks are zeroed once
+    if (!m->serve_banks_clean) {
+      if ((e = hipMemsetAsync(m->serve_sync, 0, 2 * P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
+        return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+      m->serve_banks_clean = true;
+    }
+    const unsigned bank = m->serve_epoch++ & 1u;
+    a.sync = m->serve_sync + bank * P3D_SERVE_SYNC_WORDS;
+    a.sync_next = m->serve_sync + (bank ^ 1u) * P3D_SERVE_SYNC_WORDS;
+  } else {
+    if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    m->serve_banks_clean = false;
   }
   if (use6) {
     const int T = L / 16;
@@ -2136,7 +2144,8 @@ extern "C" int p3d_serve_check(p3d_model* m) {
   if (v) {
     // reported once: the word and the sync words are cleared, so later launches are judged
     // on their own (every launch re-zeroes the sync words before it starts anyway)
-    hipMemset(m->serve_sync, 0, (P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned));
+    hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned));
+    m->serve_banks_clean = true;
     return fail(P3D_ERR_HIP, v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
                                     : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
   }

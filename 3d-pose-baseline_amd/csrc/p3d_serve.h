@@ -110,7 +110,7 @@ struct ServeArgs {
   int* err;            // set to 1 when a bounded spin ran out
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)
-  const float* ec;     // k_serve6: epilogue constants [layer][L/16 tiles][bias 16 | inv 16 | shift 16] (k_serve_prep)
+  unsigned* sync_next; // k_serve6: the other sync-word bank, zeroed by this launch for the next
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 

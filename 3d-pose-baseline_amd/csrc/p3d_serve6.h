@@ -11,6 +11,9 @@
 // each CU contracting <= 7 of a layer's 64 column tiles per phase -- 28 16x16 tiles of K = 1024
 // on the critical path and 4 phases, instead of 32 tiles and 8 phases.
 //
+// One launch per call: the sync words alternate between two banks (each launch zeroes the
+// other), the epilogue constants are formed in the prologue.
+//
 // What differs from k_serve5 (everything else -- census by hardware XCD id, flag hand-offs in
 // the XCD's L2, sc1 reads of other CUs' data, 4-wave K-split contraction with a register ring,
 // epilogue constants in LDS, steps pipelined when a group has several -- is the same design):
@@ -25,6 +28,23 @@
 #include "p3d_serve.h"
 
 #define P3D_SERVE6_RE 2            // output-reduction elements per lane (E4 / n <= 128)
+
+// Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
+// rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
+// [0] start, [1] census, [2] input layer, [3] first hand-off; per hidden phase ph at 8 ph:
+// [0] begin, [1] contraction, [2] K-combine, [3] epilogue, [4] hand-off; at 8 (NH + 1): [0]
+// the output reduction.  wall_clock64 (100 MHz).
+#ifdef P3D_TRACE
+#define P3D_S6_STAMP(row, k)                                                              \
+  do {                                                                                    \
+    if (tr6 && (row) && threadIdx.x == 0) {                                               \
+      tr6[(k)] = wall_clock64();                                                          \
+      tr6[64 + (k)] = __builtin_amdgcn_s_memtime();                                       \
+    }                                                                                     \
+  } while (0)
+#else
+#define P3D_S6_STAMP(row, k) do { } while (0)
+#endif
 
 // Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
 // rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
@@ -104,6 +124,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
 
   // ---- census: XCD id, rank within the XCD, wait for every workgroup ---------------------
+  // The sync words come in two banks used by alternate launches: this launch zeroes the
+  // other bank for the next one (stream order: the launch that used it has completed), so a
+  // launch needs no memset in front of it
+  {
+    unsigned* other = p.sync_next;
+    for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
+  }
   p3d_serve_census(p, sh, (S < 1 || S > 4) ? -1 : 64 * S);
   if (!sh[2]) {
   const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
@@ -128,7 +155,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     gi = p.nb;                               // the whole group reports instead of computing
   }
-  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;
+  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;   // (p.sync: this launch's bank)
   const int64_t slab = (int64_t)64 * L;
   float* act = p.act + (int64_t)gid * 3 * slab;
   float* part = p.part + (int64_t)gid * 2 * T * PT;
@@ -172,15 +199,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // are copied (their latencies overlap)
   f32x4 xa0[4], wb0[NCM][4];
   if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * 64, t_lo, xa0, wb0);
-  {   // epilogue constants of this member's tiles (k_serve_prep formed them)
-    const int nl = NH + 1, per = ECT * 12;   // float4s per layer
-#pragma unroll 4
-    for (int idx = tid; idx < nl * per; idx += 256) {
-      const int l = idx / per, rem = idx % per, cc = rem / 12, q = rem % 12;
-      const int t = min(t_lo + cc, T - 1);
-      *(f32x4*)(ec + (l * ECT + cc) * 48 + 4 * q) = *(const f32x4*)(p.ec + ((int64_t)l * T + t) * 48 + 4 * q);
+  {   // epilogue constants of this member's tiles, formed once per launch: bias, inv = gamma /
+      // sqrt(var + eps), shift = beta - mean * inv (the arithmetic of every other path), and
+      // each layer's max-norm divisor.  Every thread's operand loads are issued before the
+      // first is used (one round of load latency, overlapping the input layer's).
+    const int nl = NH + 1, tot = nl * ECT * 16;
+    constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 16 + 255) / 256;
+    float vb[ECN], vg[ECN], vbe[ECN], vm[ECN], vv[ECN];
+#pragma unroll
+    for (int k = 0; k < ECN; ++k) {
+      const int idx = tid + 256 * k;
+      const int l = idx / (ECT * 16), rem = idx % (ECT * 16), cs = rem >> 4, j = rem & 15;
+      const int col = 16 * min(t_lo + cs, T - 1) + j;
+      vb[k] = vg[k] = vbe[k] = vm[k] = 0.f;
+      vv[k] = 1.f;
+      if (idx < tot) {
+        const ServeLayer& lyc = p.ly[l];
+        vb[k] = lyc.bias[col];
+        if (p.bn) { vg[k] = lyc.gamma[col]; vbe[k] = lyc.beta[col]; vm[k] = lyc.mmean[col]; vv[k] = lyc.mvar[col]; }
+      }
     }
-    if (tid < nl) ecm[tid] = p.ec[(int64_t)nl * T * 48 + tid];
+    float wq = 1.f;
+    if (tid < nl && wsq_any) wq = *p.ly[tid].wsq;
+#pragma unroll
+    for (int k = 0; k < ECN; ++k) {
+      const int idx = tid + 256 * k;
+      if (idx < tot) {
+        const int l = idx / (ECT * 16), rem = idx % (ECT * 16), cs = rem >> 4, j = rem & 15;
+        float inv = 1.f, shift = 0.f;
+        if (p.bn) {
+          inv = (1.0f / sqrtf(vv[k] + p.eps)) * vg[k];
+          shift = vbe[k] - vm[k] * inv;
+        }
+        float* e = ec + (l * ECT + cs) * 48;
+        e[j] = vb[k]; e[16 + j] = inv; e[32 + j] = shift;
+      }
+    }
+    if (tid < nl) ecm[tid] = wsq_any ? fmaxf(sqrtf(wq), 1.0f) : 1.0f;
     __syncthreads();
   }
   // epilogue of tile t (chunk position cc) of layer l: z = acc / maxnorm + b, relu(z * inv + shift)

@@ -78,16 +78,30 @@ def plan_buckets(ranges, min_elems):
 
 
 def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
-    """Bucketed DP gradient average that overlaps the backward (RCCL only).
+    """Bucketed DP gradient average that overlaps the backward.
 
     For each bucket (backward order), ``comm_stream`` waits for its layer's
     gradient-ready event (``wait_ready(layer, stream_handle)``, p3d_stream_wait_grad),
-    then an async all-reduce(AVG) of that slice is issued from it; the current stream
-    finally waits for all of them.  Every byte of ``t`` is reduced exactly once, so the
-    result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).
+    then an async all-reduce(AVG) of that slice is issued from it (RCCL); the current
+    stream finally waits for all of them.  Every byte of ``t`` is reduced exactly once, so
+    the result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).  Under gloo (tests:
+    several ranks on one GPU) each bucket is copied to the host on ``comm_stream`` after
+    its event -- the same event ordering, host-staged: a bucket read before its layer's
+    gradients are final would differ from the single all-reduce.
     """
     import torch
     import torch.distributed as dist
+    if dist.get_backend() != "nccl":
+        world = dist.get_world_size()
+        with torch.cuda.stream(comm_stream):
+            for lo, hi, layer in buckets:
+                wait_ready(layer, comm_stream.cuda_stream)
+                h = t[lo:hi].to("cpu")          # synchronous on comm_stream, after the event
+                dist.all_reduce(h, op=dist.ReduceOp.SUM)
+                h.div_(world)
+                t[lo:hi].copy_(h)
+        torch.cuda.current_stream().wait_stream(comm_stream)
+        return t
     works = []
     with torch.cuda.stream(comm_stream):
         for lo, hi, layer in buckets:

@@ -234,6 +234,10 @@ class LinearModel(object):
         self.data_parallel = bool(data_parallel)
         self.rank = dist.get_rank() if self.data_parallel else 0
         self.world = dist.get_world_size() if self.data_parallel else 1
+        if self.data_parallel:   # one dropout stream for all replicas: rank 0's seed
+            obj = [self.seed]
+            dist.broadcast_object_list(obj, src=0)
+            self.seed = int(obj[0])
 
         self.train_writer = SummaryWriter(os.path.join(summaries_dir, "train"), enabled=self.rank == 0)
         self.test_writer = SummaryWriter(os.path.join(summaries_dir, "test"), enabled=self.rank == 0)
@@ -435,7 +439,12 @@ class LinearModel(object):
         (predict_3dpose.py:evaluate_batches' per-batch ``step`` loop, :396) in one persistent
         launch: each XCD runs whole steps out of its own L2 (p3d_serve, csrc/p3d_serve.h).
         Eval BN, keep_prob 1; no host sync."""
-        x = self._as_dev(x, self.input_size, "enc_in")
+        torch = self.torch
+        if not (isinstance(x, torch.Tensor) and x.dtype is torch.float32 and x.dim() == 2 and x.is_cuda
+                and x.get_device() == self.device.index and x.is_contiguous()):
+            x = self._as_dev(x, self.input_size, "enc_in")     # (the checks above: the fast path)
+        elif x.shape[1] != self.input_size:
+            raise ValueError("enc_in: expected shape [None, %d], got %s" % (self.input_size, tuple(x.shape)))
         B = x.shape[0]
         if out is None:
             out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
@@ -501,16 +510,17 @@ class LinearModel(object):
         check(lib().p3d_backward(self._h, ptr(dy), B, self.stream()), "p3d_backward")
         return loss, y
 
-    def dp_buckets(self, bucket_mb=None):
+    def dp_buckets(self, bucket_mb=None, gloo=False):
         """Enable (bucket_mb > 0) or disable (0) the bucketed gradient all-reduce that
-        overlaps the backward (RCCL only; env P3D_DP_BUCKET_MB, default 4 MB).  Must be
+        overlaps the backward (env P3D_DP_BUCKET_MB, default 4 MB; RCCL by default, gloo --
+        host-staged, for tests of several ranks on one GPU -- when gloo=True).  Must be
         called before a backward is issued.  Returns the bucket plan [(begin, end, layer)]."""
         import ctypes
         import torch.distributed as dist
         if bucket_mb is None:
             bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "4"))
         on = (bucket_mb > 0 and self.data_parallel and dist.is_initialized()
-              and dist.get_backend() == "nccl")
+              and (dist.get_backend() == "nccl" or gloo))
         check(lib().p3d_grad_events(self._h, 1 if on else 0), "p3d_grad_events")
         self._buckets = None
         if on:

@@ -292,7 +292,11 @@ def bench_serve(args, rank, world):
     # serve_check's device read runs on another queue; one more launch + synchronize puts the
     # compute queue back in the state every timed launch starts from (the first launch after
     # the read measured ~25 us slower than the median launch + synchronize round trip)
-    run(1)
+    run(int(os.environ.get("P3D_BENCH_PREWARM", "20")))
+    # and the timed region's own code once, untimed (the first pass through it measured ~10 us
+    # slower than every later one: host-side first-use costs, not GPU work)
+    barrier_sync(world)
+    run(R)
     barrier_sync(world)
     t0 = time.perf_counter()
     run(R)
@@ -310,9 +314,16 @@ def bench_serve(args, rank, world):
             t = time.perf_counter()
             fn()
             ts.append(time.perf_counter() - t)
-        return round(1e6 * sorted(ts)[len(ts) // 2], 2)
+        return round(1e6 * sorted(ts)[len(ts) // 2], 2), [round(1e6 * v, 1) for v in ts[:3]]
+    reps = []
+    for _ in range(8):     # the timed region's exact code, repeated (spread of a one-launch timing)
+        barrier_sync(world)
+        t1 = time.perf_counter()
+        run(R)
+        barrier_sync(world)
+        reps.append(round(1e6 * (time.perf_counter() - t1), 1))
     host = {"enqueue_us": med(lambda: run(1)), "launch_sync_us": med(lambda: (run(1), torch.cuda.synchronize())),
-            "idle_sync_us": med(torch.cuda.synchronize)}
+            "idle_sync_us": med(torch.cuda.synchronize), "timed_region_repeats_us": reps}
     # dominant (only) kernel, timed live: R launches, each carrying a start/stop event pair
     # attached to its dispatch (hipExtLaunchKernel), the interval rocprofv3 reports
     prof = profile_kernels(model, lambda: run(R))

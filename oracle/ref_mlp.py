@@ -449,6 +449,35 @@ def train_step(state: State, x, t, keep: float, lr0: float, seed: int = 0, ctr: 
     return loss, out
 
 
+def dp_train_step(replicas, xs, ts, keep: float, lr0: float, seed: int = 0, ctr: int | None = None,
+                  dt=np.float64):
+    """One data-parallel step of R replicas: replica r
+    runs forward + MSE + backward on its own batch xs[r] (dropout rows keyed globally, row0 =
+    r * B), the gradients are averaged over the replicas, every replica applies the same TF1
+    Adam update; BN statistics and the moving-average UPDATE_OPS stay per replica (no
+    SyncBN).  ``replicas`` share trainables and Adam slots on entry; returns the losses."""
+    if ctr is None:
+        ctr = replicas[0].global_step
+    R = len(replicas)
+    grads, losses = None, []
+    for r, st in enumerate(replicas):
+        out, cache = forward(st, xs[r], True, keep, seed, ctr, r * xs[r].shape[0], dt)
+        loss, dy = mse(out, ts[r], dt)
+        g = backward(st, cache, dy, dt)
+        grads = g if grads is None else {k: grads[k] + g[k] for k in grads}
+        bn_update(st, cache, dt)
+        losses.append(loss)
+    grads = {k: v / dt(R) for k, v in grads.items()}
+    adam_apply(replicas[0], grads, lr0, dt)
+    for st in replicas[1:]:
+        st.params.update({k: v.copy() for k, v in replicas[0].params.items()})
+        st.m = {k: v.copy() for k, v in replicas[0].m.items()}
+        st.v = {k: v.copy() for k, v in replicas[0].v.items()}
+        st.global_step = replicas[0].global_step
+        st.beta1_power, st.beta2_power = replicas[0].beta1_power, replicas[0].beta2_power
+    return losses
+
+
 def eval_step(state: State, x, t, dt=np.float64):
     """``LinearModel.step(isTraining=False)`` with keep=1 (src/linear_model.py:239-245)."""
     out, _ = forward(state, x, False, 1.0, 0, 0, 0, dt)

@@ -158,8 +158,10 @@ def test_train_steps_track_oracle(split, monkeypatch):
         t = rng.standard_normal((64, 48))
         loss, _, lr_sum, out = m.step(None, x, t, 0.5, isTraining=True)
         rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
-        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
-        close(out, ro, atol=1e-3, rtol=1e-3)
+        # measured over these 5 steps (tools/train_err_probe.py, MI355X): |d| <= 3.8e-5,
+        # loss within 7.6e-7 relative -- the tolerances keep a >= 2.5x margin
+        assert abs(loss - rl) <= 1e-5 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=1e-4, rtol=1e-4)
     gs, b1, b2 = m.get_step()
     assert gs == 5 and abs(b1 - 0.9 ** 6) < 1e-6 and abs(b2 - 0.999 ** 6) < 1e-6
     w = m.get_weights()
@@ -184,8 +186,8 @@ def test_train_steps_beyond_batch_64(B):
         t = rng.standard_normal((B, 48))
         loss, _, _, out = m.step(None, x, t, 0.5, isTraining=True)
         rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
-        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
-        close(out, ro, atol=1e-3, rtol=1e-3)
+        assert abs(loss - rl) <= 1e-5 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=2e-4, rtol=2e-4)
     w = m.get_weights()
     for name in m.trainable_names():
         if "/b1" in name or "/b2_" in name or "/b3_" in name:
@@ -223,8 +225,8 @@ def test_predict14_gradients_and_train_steps():
         t = rng.standard_normal((64, 42))
         loss, _, _, out = m.step(None, x, t, 0.5, isTraining=True)
         rl, ro = ref_mlp.train_step(st, x, t, 0.5, 1e-3, seed=m.seed, ctr=step)
-        assert abs(loss - rl) <= 2e-4 * max(1.0, rl), (step, loss, rl)
-        close(out, ro, atol=1e-3, rtol=1e-3)
+        assert abs(loss - rl) <= 1e-5 * max(1.0, rl), (step, loss, rl)
+        close(out, ro, atol=2e-4, rtol=2e-4)
     m.close()
 
 

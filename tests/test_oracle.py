@@ -234,3 +234,25 @@ def test_get_all_batches_tail_drop_and_order():
     np.testing.assert_array_equal(enc[0], d2[(9, "Walking", "a.1.h5")][:64])
     enc, dec = ref_eval.get_all_batches(d2, d3, 64, training=True, rng=np.random.default_rng(0))
     assert len(enc) == 1
+
+
+def test_dp_train_step_oracle_consistent():
+    """oracle dp_train_step: one replica == train_step; two replicas on identical batches
+    (keep 1: identical gradients) == train_step on that batch; replicas stay identical."""
+    from oracle import ref_mlp
+    cfg = ref_mlp.Cfg(linear_size=64, num_layers=1, residual=True, batch_norm=True)
+    rng = np.random.default_rng(0)
+    x, t = rng.standard_normal((16, 32)), rng.standard_normal((16, 48))
+    a = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
+    b = a.copy()
+    reps = [a.copy(), a.copy()]
+    ref_mlp.train_step(a, x, t, 0.5, 1e-3, seed=3, ctr=0)
+    ref_mlp.dp_train_step([b], [x], [t], 0.5, 1e-3, seed=3, ctr=0)
+    for k in a.params:
+        np.testing.assert_array_equal(a.params[k], b.params[k])
+    c = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
+    ref_mlp.train_step(c, x, t, 1.0, 1e-3, seed=3, ctr=0)
+    ref_mlp.dp_train_step(reps, [x, x], [t, t], 1.0, 1e-3, seed=3, ctr=0)
+    for k in c.params:
+        np.testing.assert_allclose(reps[0].params[k], c.params[k], rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(reps[0].params[k], reps[1].params[k])
