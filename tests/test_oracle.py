@@ -12,6 +12,7 @@ import torch
 from oracle import ref_eval, ref_mlp
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.npz")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -256,3 +257,23 @@ def test_dp_train_step_oracle_consistent():
     for k in c.params:
         np.testing.assert_allclose(reps[0].params[k], c.params[k], rtol=1e-6, atol=1e-7)
         np.testing.assert_array_equal(reps[0].params[k], reps[1].params[k])
+
+
+def test_cfg4_fixture_matches_its_generator():
+    """tests/golden/cfg4_oracle.npz (the oracle's per-action MPJPE of the cfg4 sweep, used by
+    tests/test_gpu_eval_cfg4.py) was made from cfg4_data.make_cfg4_set: same actions, same
+    tail-dropped frame counts (494,784 in all, bench.py's eval_sweep draw)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from cfg4_data import ACTIONS, make_cfg4_set
+    from oracle import ref_eval
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cfg4_oracle.npz"), allow_pickle=False)
+    assert list(g["actions"]) == ACTIONS == ref_eval.define_actions("All")
+    s2, s3 = make_cfg4_set()
+    for a, n in zip(ACTIONS, g["frames"]):
+        enc, _ = ref_eval.get_all_batches(ref_eval.get_action_subset(s2, a), ref_eval.get_action_subset(s3, a), 64,
+                                          camera_frame=True, training=False)
+        assert 64 * len(enc) == int(n), a
+    assert int(g["frames"].sum()) == 494784
+    counts = np.random.default_rng(4).integers(20000, 40001, 15)   # bench.py bench_eval's draw
+    assert int(sum(int(c) // 64 for c in counts)) * 64 == 494784
