@@ -28,7 +28,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cstdlib>
+#include <mutex>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 // =====================================================================================
@@ -1292,6 +1295,48 @@ void free_all(p3d_model* m) {
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
 }
+// ---- teardown in any order -------------------------------------------------------------
+// A model's device memory must go while the HIP runtime is alive and nothing still runs on
+// it.  p3d_destroy synchronises the device before freeing (kernels of an aborted step may
+// still be queued), and the first p3d_create registers a process-exit handler that releases
+// every model still alive.  That handler runs before the HIP runtime's own teardown (exit
+// handlers run in reverse order of registration, and the runtime registered its own when it
+// was initialised, before any model existed); a p3d_destroy arriving after it -- a Python
+// finaliser during interpreter teardown -- finds the model gone and touches nothing.
+std::mutex g_live_mu;
+std::unordered_set<p3d_model*>* g_live = nullptr;
+bool g_exit_hooked = false;
+
+void release_model(p3d_model* m) {
+  (void)hipDeviceSynchronize();
+  for (hipEvent_t e : m->gev) (void)hipEventDestroy(e);
+  free_all(m);
+  delete m;
+}
+
+void release_live_models_at_exit() {
+  std::unordered_set<p3d_model*> live;
+  {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (g_live) live.swap(*g_live);
+  }
+  for (p3d_model* m : live) release_model(m);
+}
+
+void live_models_add(p3d_model* m) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (!g_live) g_live = new std::unordered_set<p3d_model*>();
+  g_live->insert(m);
+  if (!g_exit_hooked) {
+    g_exit_hooked = true;
+    std::atexit(release_live_models_at_exit);
+  }
+}
+
+bool live_models_remove(p3d_model* m) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  return g_live && g_live->erase(m) > 0;
+}
 }  // namespace
 
 extern "C" const char* p3d_last_error(void) { return g_err.c_str(); }
@@ -1515,15 +1560,15 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     if ((e = hipMalloc(&m->abf, (int64_t)(nl + 1) * slab * 2)) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->abf, 0, (int64_t)(nl + 1) * slab * 2)) != hipSuccess) return cleanup(e);
   }
+  live_models_add(m);
   *out = m;
   return P3D_OK;
 }
 
 extern "C" int p3d_destroy(p3d_model* m) {
   if (!m) return P3D_OK;
-  for (hipEvent_t e : m->gev) (void)hipEventDestroy(e);
-  free_all(m);
-  delete m;
+  if (!live_models_remove(m)) return P3D_OK;   // released already (process exit)
+  release_model(m);
   return P3D_OK;
 }
 

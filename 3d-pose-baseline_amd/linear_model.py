@@ -15,31 +15,16 @@ fallback: construction fails if libp3d.so cannot be loaded.
 """
 from __future__ import annotations
 
-import atexit
 import json
 import math
 import os
 import time
-import weakref
 
 import numpy as np
 
 import _p3d
 import dist_utils
 from _p3d import check, lib, ptr
-
-# Models still open at interpreter exit are destroyed here, before the HIP runtime is torn
-# down (a p3d_destroy from a __del__ during teardown has crashed the process).
-_LIVE = weakref.WeakSet()
-
-
-@atexit.register
-def _close_live_models():
-    for m in list(_LIVE):
-        try:
-            m.close()
-        except Exception:
-            pass
 
 HUMAN_2D_SIZE = 16 * 2
 
@@ -216,7 +201,6 @@ class LinearModel(object):
         with torch.cuda.device(self.device):
             check(lib().p3d_create(_p3d.ctypes.byref(cfg), _p3d.ctypes.byref(h)), "p3d_create")
         self._h = h
-        _LIVE.add(self)
         self._tables()
 
         # placeholders / tensors the reference exposes (src/linear_model.py:77-134)
