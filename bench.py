@@ -292,7 +292,10 @@ def bench_serve(args, rank, world):
     # serve_check's device read runs on another queue; one more launch + synchronize puts the
     # compute queue back in the state every timed launch starts from (the first launch after
     # the read measured ~25 us slower than the median launch + synchronize round trip)
-    run(int(os.environ.get("P3D_BENCH_PREWARM", "20")))
+    # ~100 launches (~15 ms) of pre-warm: the chip's clock ramps under this load -- launch
+    # durations fall from ~152 to ~136 us over the first ~80 launches
+    # (profiles/r02_v1_serve_launches.json); with 20 the timed launch ran at ~146 us
+    run(int(os.environ.get("P3D_BENCH_PREWARM", "100")))
     # and the timed region's own code, untimed (the first pass through it measured ~10 us
     # slower than every later one: host-side first-use costs, not GPU work)
     for _ in range(3):
