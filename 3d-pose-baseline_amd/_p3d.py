@@ -48,6 +48,7 @@ SIGNATURES = [
                                  c_uint64, c_int64, c_int64, c_void_p]),
     ("p3d_serve", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("p3d_serve_check", c_int32, [c_void_p]),
+    ("p3d_sync_check", c_int32, [c_void_p]),
     ("p3d_mse", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_backward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_adam_step", c_int32, [c_void_p, c_float, c_void_p]),

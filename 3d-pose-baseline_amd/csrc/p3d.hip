@@ -21,6 +21,8 @@
 #include "p3d_data.h"
 #include "p3d_serve.h"
 #include "p3d_serve6.h"
+#include "p3d_gemv.h"
+#include "p3d_xchg.h"
 #include "../../include/p3d.h"
 
 #include <math.h>
@@ -163,6 +165,7 @@ struct FwdArgs {
   float* dy; float dscale;        //   dy = dscale * (y - t) stored row-major (leading dim lddy),
   int64_t lddy;
   float* lossp;                   //   per-workgroup sum of (y - t)^2
+  XchgSite xs;                    // bn == 4 (BN-train exchange form, p3d_xchg.h)
 };
 
 // Phase timestamps for kernel development (build with -DP3D_TRACE; tools/trace_train.py).
@@ -208,7 +211,9 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
   uint64_t ctr = p.ctr;
+  unsigned xtag = 0;
   if (w == 0) {
+    if (p.bn == 4) xtag = p3d_xchg_tag(p.xs);
     if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     b = p.bias[cc];
     if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
@@ -240,10 +245,12 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) z[s][r] = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + b;
 
-  if (p.bn == 3) {
-    // BN-train, split form (k_bn_fwd finishes the layer): z and this row tile's per-column
-    // count-weighted moments {sum, M2 about the tile mean} for Chan's combination
-    float sum = 0.f;
+  float xmean = 0.f, xvar = 1.f, sum = 0.f, sq = 0.f, uu_x[RS][4];
+  if (p.bn == 3 || p.bn == 4) {
+    // BN-train: this row tile's per-column count-weighted moments {sum, M2 about the tile
+    // mean} for Chan's combination.  Split form (bn = 3): z and the moments out, k_bn_fwd
+    // finishes the layer.  Exchange form (bn = 4): the row-tile siblings swap their moments
+    // here (p3d_xchg.h) and every workgroup finishes its own tile below.
 #pragma unroll
     for (int s = 0; s < RS; ++s)
 #pragma unroll
@@ -252,13 +259,37 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     sum = p3d_colsum16(sum);
     const int nt = min(16 * RS, p.M - m0);
     const float mt = sum / (float)nt;
-    float sq = 0.f;
 #pragma unroll
     for (int s = 0; s < RS; ++s)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mt; sq += d * d; }
     sq = p3d_colsum16(sq);
+    if (p.bn == 4) {
+      const int R = (int)gridDim.y;
+      float st[P3D_XCHG_MAXR], qt[P3D_XCHG_MAXR];
+      p3d_xchg_put(p.xs, p.N, blockIdx.y, col, q == 0 && cok, sum, sq, xtag);
+      // the dropout uniforms do not depend on the statistics: formed while the siblings arrive
+      if (p.keep < 1.0f) {
+#pragma unroll
+        for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu_x[s]);
+      }
+      p3d_xchg_get(p.xs, p.N, R, cc, xtag, st, qt);
+      p3d_xchg_done(p.xs, blockIdx.y);
+      float S = 0.f;
+#pragma unroll
+      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
+        if (t < R) S += st[t];
+      const float fm = (float)p.M;
+      xmean = S / fm;
+      float M2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
+        if (t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, p.M - 16 * t), xmean);
+      xvar = M2 / fm;
+    }
+  }
+  if (p.bn == 3) {
     if (!cok) return;
     if (q == 0) {
       p.bnpart[((int64_t)blockIdx.y * p.N + col) * 2] = sum;
@@ -274,7 +305,15 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     return;
   }
   float inv = 1.0f, shift = 0.0f;
-  if (p.bn) {
+  if (p.bn == 4) {
+    p3d_bn_affine(xmean, xvar, p.eps, gam, bet, inv, shift);
+    if (blockIdx.y == 0 && q == 0 && cok) {
+      p.mean_save[col] = xmean;
+      p.var_save[col] = xvar;
+      p.mmean[col] = p3d_bn_moving(mmu, xmean, p.decay);
+      p.mvar[col] = p3d_bn_moving(mva, xvar, p.decay);
+    }
+  } else if (p.bn) {
     float mean = mmu, var = mva;
     if (p.bn == 2) {  // batch statistics over all M rows (host guarantees M <= 16*RS)
       float sum = 0.f;
@@ -307,7 +346,14 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   float uu[RS][4];
   if (p.keep < 1.0f) {
 #pragma unroll
-    for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu[s]);
+    for (int s = 0; s < RS; ++s) {
+      if (p.bn == 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) uu[s][r] = uu_x[s][r];
+      } else {
+        p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu[s]);
+      }
+    }
   }
   if (trace) P3D_STAMP(4);
   if (p.tgt) {
@@ -336,7 +382,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
       if (p.z_save) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
-      float y = p.bn ? z[s][r] * inv + shift : z[s][r];
+      float y = p.bn == 4 ? p3d_bn_y(z[s][r], inv, shift) : p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
       if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, uu[s][r]);
       if (p.res) y += rv[s][r];
@@ -510,23 +556,17 @@ __global__ __launch_bounds__(64) void k_bn_fwd(BnFwdArgs p) {
     float M2 = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      if (t < R) {
-        const int nt = min(16, p.M - 16 * t);
-        const float d = pp[t][e >> 1][(e & 1) * 2] / (float)nt - mean;
-        M2 += pp[t][e >> 1][(e & 1) * 2 + 1] + (float)nt * d * d;
-      }
+      if (t < R) M2 += p3d_chan_term(pp[t][e >> 1][(e & 1) * 2], pp[t][e >> 1][(e & 1) * 2 + 1], min(16, p.M - 16 * t), mean);
     for (int t = 4; t < R; ++t) {
-      const int nt = min(16, p.M - 16 * t);
       const float* pt = p.part + ((int64_t)t * p.N + n0 + e) * 2;
-      const float d = pt[0] / (float)nt - mean;
-      M2 += pt[1] + (float)nt * d * d;
+      M2 += p3d_chan_term(pt[0], pt[1], min(16, p.M - 16 * t), mean);
     }
     const float var = M2 / fm;
     mean4[e] = mean;
     var4[e] = var;
-    const float inv = (1.0f / sqrtf(var + p.eps)) * g4[e];
-    const float shift = b4[e] - mean * inv;
-    float y = z4[e] * inv + shift;
+    float inv, shift;
+    p3d_bn_affine(mean, var, p.eps, g4[e], b4[e], inv, shift);
+    float y = p3d_bn_y(z4[e], inv, shift);
     if (p.relu) y = fmaxf(y, 0.0f);
     if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, u[e]);
     if (p.res) y += r4[e];
@@ -539,8 +579,8 @@ __global__ __launch_bounds__(64) void k_bn_fwd(BnFwdArgs p) {
     f32x4 nm, nv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      nm[e] = mm4[e] - (mm4[e] - mean4[e]) * p.decay;
-      nv[e] = mv4[e] - (mv4[e] - var4[e]) * p.decay;
+      nm[e] = p3d_bn_moving(mm4[e], mean4[e], p.decay);
+      nv[e] = p3d_bn_moving(mv4[e], var4[e], p.decay);
     }
     *(f32x4*)(p.mmean + n0) = nm;
     *(f32x4*)(p.mvar + n0) = nv;
@@ -569,6 +609,7 @@ struct BwdArgs {
                                   // dz then holds g (k_bn_bwd finishes it)
   const float* lossp; int nlossp; // fused MSE: workgroup 0 folds the forward's loss partials
   float* loss; float loss_scale;  //   (fixed order) into loss[0] = scale * sum
+  XchgSite xs; int xchg;          // with bnpart: exchange form (p3d_xchg.h) -- dz, dgamma, dbeta here
 };
 
 // RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
@@ -591,7 +632,9 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   // prefetch the epilogue's per-column and per-element operands
   float mean = 0.f, var = 1.f, gam = 1.f, bet = 0.f, zz[RS][4], dr[RS][4];
   uint64_t ctr = p.ctr;
+  unsigned xtag = 0;
   if (w == 0) {
+    if (p.xchg) xtag = p3d_xchg_tag(p.xs);
     if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     if (p.prev && p.bn) { mean = p.mean[cc]; var = p.var[cc]; gam = p.gamma[cc]; bet = p.beta[cc]; }
 #pragma unroll
@@ -658,6 +701,29 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   if (p.bn) {
     sg = p3d_colsum16(sg);
     sgx = p3d_colsum16(sgx);
+    if (p.xchg) {   // exchange form: the row-tile siblings swap {sum g, sum g xhat}
+      const int R = (int)gridDim.y;
+      float at[P3D_XCHG_MAXR], bt[P3D_XCHG_MAXR];
+      p3d_xchg_put(p.xs, p.K, blockIdx.y, col, q == 0 && cok, sg, sgx, xtag);
+      p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt);
+      p3d_xchg_done(p.xs, blockIdx.y);
+      sg = 0.f;
+      sgx = 0.f;
+#pragma unroll
+      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
+        if (t < R) { sg += at[t]; sgx += bt[t]; }
+      if (!cok) return;
+      if (blockIdx.y == 0 && q == 0) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
+      const float fmx = (float)p.M;
+#pragma unroll
+      for (int s = 0; s < RS; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + 16 * s + 4 * q + r;
+          if (row < p.M) p.dz[p3d_pk(row, col, ngK)] = p3d_bn_dz(inv, fmx, g[s][r], sg, xh[s][r], sgx);
+        }
+      return;
+    }
     if (p.bnpart) {   // split form: partials + g; k_bn_bwd forms dz, dgamma, dbeta
       if (!cok) return;
       if (q == 0) {
@@ -683,7 +749,7 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
-      const float dz = p.bn ? (inv / fm) * (fm * g[s][r] - sg - xh[s][r] * sgx) : g[s][r];
+      const float dz = p.bn ? p3d_bn_dz(inv, fm, g[s][r], sg, xh[s][r], sgx) : g[s][r];
       p.dz[p3d_pk(row, col, ngK)] = dz;
     }
 }
@@ -733,7 +799,7 @@ __global__ __launch_bounds__(64) void k_bn_bwd(BnBwdArgs p) {
     const float rstd = 1.0f / sqrtf(va4[e] + p.eps);
     const float inv = rstd * ga4[e];
     const float xh = (z4[e] - mu4[e]) * rstd;
-    o[e] = row < p.M ? (inv / fm) * (fm * g4[e] - sg - xh * sgx) : 0.0f;
+    o[e] = row < p.M ? p3d_bn_dz(inv, fm, g4[e], sg, xh, sgx) : 0.0f;
   }
   *(f32x4*)(p.dz + off) = o;
   if (rt == 0 && j == 0) {
@@ -1188,6 +1254,11 @@ struct p3d_model {
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
+  int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
+  int num_cus = 0;            // compute units of the device (exchange-form residency bound)
+  unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) an epoch word (own 128-B line), then
+                              // the error word, then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
+  int* xerr = nullptr;        // set when an in-launch synchronisation timed out (p3d_sync_check)
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
   float* aff = nullptr;             // BN-eval affine per BN layer
@@ -1226,6 +1297,7 @@ struct p3d_model {
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
+  int gemv_maxb = 4;        // inference at B <= gemv_maxb runs the k_gemv layers (env P3D_GEMV_MAXB, 0..4)
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
@@ -1294,6 +1366,7 @@ void free_all(p3d_model* m) {
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
+  if (m->xsync) (void)hipFree(m->xsync);
 }
 // ---- teardown in any order -------------------------------------------------------------
 // A model's device memory must go while the HIP runtime is alive and nothing still runs on
@@ -1507,8 +1580,20 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_BIG")) m->out_big = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
+  if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
+  if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
+  {
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return cleanup(e);
+    if ((e = hipDeviceGetAttribute(&m->num_cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+      return cleanup(e);
+    const int64_t nx = (int64_t)(2 * nl + 1) * 32 + (int64_t)2 * nl * P3D_XCHG_MAXR * L * 4;
+    if ((e = hipMalloc(&m->xsync, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    if ((e = hipMemset(m->xsync, 0, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    m->xerr = (int*)(m->xsync + 2 * nl * 32);
+  }
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
@@ -1715,10 +1800,34 @@ static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
 
 // BN-train layer, split form: 16x16 GEMM tiles (256 workgroups at L = 1024, B = 64) write z
 // and row-tile moments, then k_bn_fwd applies batch-stat BN / ReLU / dropout / residual.
+// The exchange form (p3d_xchg.h: one launch, the row-tile siblings swap their BN partials)
+// needs every workgroup of the grid resident at once: one per CU at most, <= 16 row tiles.
+static bool use_xchg(const p3d_model* m, int N, int M) {
+  const int gx = (N + 15) / 16, gy = (M + 15) / 16;
+  return m->train_xchg && gy <= P3D_XCHG_MAXR && gx * gy <= m->num_cus;
+}
+static XchgSite xchg_site(const p3d_model* m, int slot) {
+  const int nl = (int)m->layers.size();
+  XchgSite x;
+  x.epoch = m->xsync + (int64_t)slot * 32;
+  x.slots = (float*)(m->xsync + (int64_t)(2 * nl + 1) * 32) + (int64_t)slot * P3D_XCHG_MAXR * m->cfg.linear_size * 4;
+  x.err = m->xerr;
+  return x;
+}
+
 static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
   FwdArgs a = a0;
   a.bn = 3; a.bnpart = m->bnpart;
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
+  if (use_xchg(m, a.N, a.M)) {   // BN-train layer as ONE launch
+    a.bn = 4; a.xs = xchg_site(m, a.site);
+    static const char* tags[2] = {"fwd_in_train_x", "fwd_hidden_train_x"};
+    ProfScope ps(m, tags[kind == 0 ? 0 : 1]);
+    if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, grid, dim3(512), st, a);
+    else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, grid, dim3(512), st, a);
+    LAUNCH_CHECK("k_fwd");
+    return P3D_OK;
+  }
   {
     static const char* tags[3] = {"fwd_in_train_z", "fwd_hidden_train_z", "fwd_out_train_z"};
     ProfScope ps(m, tags[kind]);
@@ -1869,6 +1978,47 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
   return P3D_OK;
 }
 
+// Batch <= 4 inference (p3d_gemv.h): every layer as one weight-streaming k_gemv launch.
+static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float keep_prob, uint64_t seed,
+                        uint64_t ctr, int64_t row_offset, int64_t wsoff, hipStream_t st) {
+  const p3d_cfg& c = m->cfg;
+  const int nl = (int)m->layers.size();
+  const float* in = x;
+  for (int l = 0; l < nl; ++l) {
+    const Layer& ly = m->layers[l];
+    const bool last = (l == nl - 1);
+    GemvArgs a{};
+    a.X = in; a.ldx = c.input_size; a.xpk = l > 0;
+    a.Wf = m->wpk + ly.wf;
+    a.bias = m->flat[0] + ly.b;
+    a.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
+    a.M = (int)B; a.K = ly.K; a.N = ly.N;
+    if (ly.bn) {
+      a.bn = 1;
+      a.gamma = m->flat[0] + ly.gamma; a.beta = m->flat[0] + ly.beta;
+      a.mmean = m->moving + ly.mmean; a.mvar = m->moving + ly.mvar;
+      a.eps = c.bn_eps;
+    }
+    a.relu = ly.relu;
+    a.keep = last ? 1.0f : keep_prob;
+    a.seed = seed; a.ctr = ctr; a.site = ly.site; a.row_off = row_offset;
+    a.ctr_dev = (ctr == P3D_CTR_GLOBAL_STEP) ? &m->dstate->global_step : nullptr;
+    const bool second = (l >= 1 && !last && ((l - 1) % 2 == 1));
+    if (c.residual && second) a.res = m->act[l - 2] + wsoff;
+    if (last) { a.Y = y; a.ldy = ly.N; a.ypk = 0; }
+    else { a.Y = m->act[l] + wsoff; a.ldy = 0; a.ypk = 1; }
+    const dim3 grid((unsigned)((ly.N + 15) / 16));
+    {
+      ProfScope ps(m, l == 0 ? "gemv_in" : (last ? "gemv_out" : "gemv_hidden"));
+      if (l == 0) go(ps, k_gemv<4, 2, 4>, grid, dim3(128), st, a);
+      else go(ps, k_gemv<4, 16, 4>, grid, dim3(1024), st, a);
+    }
+    LAUNCH_CHECK("k_gemv");
+    in = a.Y;
+  }
+  return P3D_OK;
+}
+
 static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32_t training, float keep_prob,
                         uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row, void* stream,
                         const float* tgt);
@@ -1906,6 +2056,7 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
   const float decay = 1.0f - c.bn_momentum;
   const int nl = (int)m->layers.size();
   const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
+  if (!training && !tgt && B <= m->gemv_maxb) return forward_gemv(m, x, B, y, keep_prob, seed, ctr, row_offset, wsoff, st);
   const float* in = x;
   for (int l = 0; l < nl; ++l) {
     const Layer& ly = m->layers[l];
@@ -2189,10 +2340,24 @@ extern "C" int p3d_serve_check(p3d_model* m) {
   if (v) {
     // reported once: the word and the sync words are cleared, so later launches are judged
     // on their own (every launch re-zeroes the sync words before it starts anyway)
-    hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned));
+    if ((e = hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
     m->serve_banks_clean = true;
     return fail(P3D_ERR_HIP, v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
                                     : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
+  }
+  return P3D_OK;
+}
+
+extern "C" int p3d_sync_check(p3d_model* m) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  int v = 0;
+  hipError_t e = hipMemcpy(&v, m->xerr, sizeof(int), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_sync_check: ") + hipGetErrorString(e));
+  if (v) {
+    if ((e = hipMemset(m->xerr, 0, sizeof(int))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_sync_check: ") + hipGetErrorString(e));
+    return fail(P3D_ERR_HIP, "p3d_sync_check: a BN-train exchange timed out (row-tile workgroups not all resident)");
   }
   return P3D_OK;
 }
@@ -2357,6 +2522,10 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
     if (m->train_split) {
       if (pv.bn) a.bnpart = m->bnpart;
+      // (not while gradient-ready events feed a concurrent all-reduce: its kernels hold CUs
+      // the exchange's siblings need resident together)
+      const bool xchg = pv.bn && use_xchg(m, a.K, a.M) && m->gev.empty();
+      if (xchg) { a.xchg = 1; a.xs = xchg_site(m, nl + l - 1); }   // dz, dgamma, dbeta here
       const dim3 grid((a.K + 15) / 16, (a.M + 15) / 16);
       {
         ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
@@ -2364,7 +2533,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         else go(ps, k_dgrad<1, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
       }
       LAUNCH_CHECK("k_dgrad");
-      if (pv.bn) {
+      if (pv.bn && !xchg) {
         BnBwdArgs b{};
         b.dz = a.dz; b.z = a.z; b.part = m->bnpart; b.M = a.M; b.K = a.K;
         b.mean = a.mean; b.var = a.var; b.gamma = a.gamma; b.eps = a.eps;
@@ -2573,7 +2742,8 @@ extern "C" int p3d_mpjpe_accum(const float* pred_n, const float* gt_n, const dou
 
 // rocprofv3 name of the kernel a launch of `what` uses under the current tiling variants:
 // 0 = inference hidden layer at B <= 64 (bench.py's roofline kernel), 1 = inference hidden
-// layer at large M, 2 = BN-train hidden GEMM.
+// layer at large M, 2 = BN-train hidden GEMM, 3 = the last p3d_serve kernel, 4 = inference hidden
+// layer at batch <= 4 (k_gemv).
 extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len) {
   if (!m || !out || out_len <= 0) return fail(P3D_ERR_ARG, "p3d_kernel_name: bad argument");
   std::string n;
@@ -2615,6 +2785,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
           std::to_string(ks) + ">";
   } else if (what == 2) {
     n = m->train_split ? "k_fwd<1, 8, 8, 2, true, true, 1>" : "k_fwd<4, 8, 8, 2, true, true, 1>";
+  } else if (what == 4) {
+    n = "k_gemv<4, 16, 4>";   // inference hidden layer at B <= gemv_maxb
   } else {
     return fail(P3D_ERR_ARG, "p3d_kernel_name: unknown kernel selector");
   }

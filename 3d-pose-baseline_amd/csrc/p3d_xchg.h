@@ -1,0 +1,121 @@
+// p3d_xchg.h -- batch-norm training layers as ONE launch (gfx950).
+//
+// tf.layers.batch_normalization in training mode (src/linear_model.py:112,181,193) needs each
+// column's mean / variance over the whole batch before any output element of that column can
+// be formed; the backward needs the column sums of g and g * xhat the same way.  The GEMM of a
+// layer runs as 16 x 16 tiles, so a column's B = 64 rows sit in R = 4 row-tile workgroups.
+//
+// Split form (k_fwd bn = 3 + k_bn_fwd, k_dgrad + k_bn_bwd): the GEMM stores z and per-tile
+// moments, a second launch combines them -- one extra dependent launch per BN layer and
+// direction (~4.4 us each at cfg3, 10 per step).
+//
+// Exchange form (this file): the R row-tile workgroups of a column tile swap their per-column
+// partials inside the GEMM launch and each finishes its own tile.  The partials travel as
+// data-tagged granules (the R2 form of cdna_hip_programming.md Guideline 16: the data IS the
+// flag, no flag word, no fence, no drain before a signal):
+//   1. at kernel start lane 0 of wave 0 reads the site's epoch word (agent-scope load); the
+//      launch's tag is epoch + 1;
+//   2. after the GEMM, wave 0 stores its 16 columns' pairs as {a, tag, b, tag} 16-B write-through
+//      (sc1) stores into this site's slot array, one 256-B run per workgroup;
+//   3. wave 0 re-reads the R siblings' 16-B entries of its column with sc1 loads (L1 bypassed)
+//      until every tag equals this launch's (bounded spin, s_sleep between sweeps), and combines
+//      them in row-tile order -- the association of the split form's second kernel, so both
+//      forms give the same bits (the helpers below are shared and compiled without FMA
+//      contraction);
+//   4. the row-tile-0 workgroup, once it has read every sibling's entry, adds 1 to the epoch
+//      word (agent atomic, no return).  Every sibling read the epoch before publishing, and
+//      row tile 0 adds only after it has seen all of them, so the epoch changes only after
+//      every sibling of this launch holds its tag: each launch's tag is unique without a
+//      memset in front (graph replays included), stale entries of earlier launches never match.
+// Each site (layer and direction) has its own epoch word and slot array.  The siblings of a
+// column tile have equal blockIdx % 8, i.e. one XCD under the observed round-robin placement
+// (speed only, never correctness).  Every sibling must be resident at once: the host uses this
+// form only when the grid fits on the device's CUs at one workgroup each.  Every spin is
+// bounded (~0.5 s) and sets *err (p3d_sync_check) instead of hanging the GPU.
+#pragma once
+#include "p3d_kernels.h"
+
+#define P3D_XCHG_MAXR 16          // row tiles per exchange (B <= 256)
+#define P3D_XCHG_SPIN (1 << 19)
+
+// ---- arithmetic shared by the split and exchange forms (no FMA contraction) -------------
+// BN affine of TF1's non-fused batch norm: inv = rsqrt(var + eps) * gamma, shift = beta - mean * inv
+__device__ __forceinline__ void p3d_bn_affine(float mean, float var, float eps, float gam, float bet, float& inv,
+                                              float& shift) {
+#pragma clang fp contract(off)
+  inv = (1.0f / sqrtf(var + eps)) * gam;
+  shift = bet - mean * inv;
+}
+__device__ __forceinline__ float p3d_bn_y(float z, float inv, float shift) {
+#pragma clang fp contract(off)
+  return z * inv + shift;
+}
+// UPDATE_OPS moving average (momentum 0.99): m - (m - stat) * (1 - momentum)
+__device__ __forceinline__ float p3d_bn_moving(float m, float stat, float decay) {
+#pragma clang fp contract(off)
+  return m - (m - stat) * decay;
+}
+// Chan's combination, one row tile's term: M2_t + n_t * (mean_t - mean)^2
+__device__ __forceinline__ float p3d_chan_term(float s_t, float q_t, int nt, float mean) {
+#pragma clang fp contract(off)
+  const float d = s_t / (float)nt - mean;
+  return q_t + (float)nt * d * d;
+}
+// BN-train data gradient: dz = inv / M * (M g - sum g - xhat * sum g xhat)
+__device__ __forceinline__ float p3d_bn_dz(float inv, float fm, float g, float sg, float xh, float sgx) {
+#pragma clang fp contract(off)
+  return (inv / fm) * (fm * g - sg - xh * sgx);
+}
+
+// ---- the exchange ------------------------------------------------------------------------
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+struct XchgSite {
+  unsigned* epoch;   // one word (own 128-B line)
+  float* slots;      // [P3D_XCHG_MAXR row tiles][N columns] 16-B entries {a, tag, b, tag}
+  int* err;
+};
+
+// This launch's tag (wave-uniform; read at kernel start so its latency hides under the GEMM).
+__device__ __forceinline__ unsigned p3d_xchg_tag(const XchgSite& x) {
+  return __hip_atomic_load(x.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// Wave 0, all 64 lanes: lanes with `mine` publish their column's pair (write-through).
+__device__ __forceinline__ void p3d_xchg_put(const XchgSite& x, int N, int rt, int col, bool mine, float a0, float b0,
+                                             unsigned tag) {
+  if (mine) {
+    const u32x4_t v = {__float_as_uint(a0), tag, __float_as_uint(b0), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, p3d_rsrc(x.slots), (rt * N + col) * 16, 0, 16);   // aux 16 = sc1
+  }
+}
+
+// Wave 0, all 64 lanes: every lane collects the R pairs of column `col` (a[t], b[t], t < R)
+// once all R tags match (independent work of the caller can sit between put and get).
+__device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, int col, unsigned tag,
+                                             float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR]) {
+  const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(x.slots);
+  for (int spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int t = 0; t < P3D_XCHG_MAXR; ++t)
+      if (t < R) {
+        const u32x4_t v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (t * N + col) * 16, 0, 16));
+        a[t] = __uint_as_float(v.x);
+        b[t] = __uint_as_float(v.z);
+        ok &= (v.y == tag) & (v.w == tag);
+      }
+    if (__all(ok)) break;
+    if (spin > P3D_XCHG_SPIN) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Row tile 0, after its swap: the next launch of this site gets a new tag.
+__device__ __forceinline__ void p3d_xchg_done(const XchgSite& x, int rt) {
+  if (rt == 0 && (threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(x.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -439,6 +439,10 @@ class LinearModel(object):
         """Raise if a p3d_serve launch could not synchronise its workgroups (device read)."""
         check(lib().p3d_serve_check(self._h), "p3d_serve")
 
+    def sync_check(self):
+        """Raise if a BN-train layer's in-launch exchange timed out (device read)."""
+        check(lib().p3d_sync_check(self._h), "p3d_train")
+
     def loss_device(self, y, t, dy=None):
         B = y.shape[0]
         check(lib().p3d_mse(ptr(y), ptr(t), B, self.output_size, ptr(self._loss_dev),

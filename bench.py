@@ -649,6 +649,39 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
     dt = time.perf_counter() - t0
     out["eval_b1"] = {"us_per_call": round(1e6 * dt / n1, 2), "unit": "us",
                       "note": "LinearModel.step() at batch 1 from numpy: H2D, 6 layer kernels, MSE, D2H, sync"}
+    # device time of the batch-1 forward itself (k_gemv layers): a HIP graph of 50 forwards
+    # replayed back to back (kernels + the dependent boundaries between them), and the hidden
+    # layer's dispatch-attached duration against its weight stream
+    x1d = torch.from_numpy(xs[0][:1].astype(np.float32)).cuda()
+    y1d = torch.empty((1, OUT), dtype=torch.float32, device="cuda")
+    fwd1 = lambda: model.forward_device(x1d, False, 1.0, out=y1d, ctr=0)   # noqa: E731
+    for _ in range(20):
+        fwd1()
+    torch.cuda.synchronize()
+    g1 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1):
+        for _ in range(50):
+            fwd1()
+    for _ in range(5):
+        g1.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        g1.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    dev_us = 1000.0 * e0.elapsed_time(e1) / 500
+    prof = profile_kernels(model, lambda: [fwd1() for _ in range(100)])
+    hb = 4 * (L * L + 5 * L) + 4 * 3 * L          # weights + bias/BN vectors + x, residual, y
+    h_us = prof["gemv_hidden"][1]
+    out["forward_b1"] = {
+        "us_per_forward": round(dev_us, 2), "unit": "us",
+        "note": "device time of one batch-1 forward (6 k_gemv launches), graph of 50 replayed back to back",
+        "layers_us": {k: round(v[1], 3) for k, v in prof.items()},
+        "roofline": {"bound": "hbm", "kernel": kernel_name(model, 4) + " (hidden layer, batch 1)",
+                     "bytes_per_launch": hb, "avg_us": round(h_us, 3),
+                     "achieved": round(hb / (h_us * 1e-6) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(hb / (h_us * 1e-6) / 1e9 / 8000.0, 4), "traffic": None}}
     # the front end's whole per-frame path as one graph (openpose_frontend.FrameLifter):
     # pinned H2D of the mapped frame, normalise, 6 layers, unNormalizeData, D2H
     import data_utils
@@ -673,9 +706,11 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
     return out
 
 
-def bench_stress(args, rank, world):
+def bench_stress(args, rank, world, steps=None, warmup=None):
     """cfg5: L=4096, 4 residual blocks, bf16 weights/activations with fp32 accumulate and
     fp32 BN, batch 1024, inference.  One step = one forward of one batch of 1024 poses."""
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     import torch
     import _p3d
     import linear_model
@@ -705,8 +740,8 @@ def bench_stress(args, rank, world):
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         run(G)
-    steps = max(G, args.steps // G * G)
-    for _ in range(max(1, args.warmup // G)):
+    steps = max(G, steps // G * G)
+    for _ in range(max(1, warmup // G)):
         graph.replay()
     barrier_sync(world)
     t0 = time.perf_counter()
@@ -887,6 +922,8 @@ def main():
     ap.add_argument("--no-api", action="store_true", help="skip the LinearModel.step() API-level rates (infer mode)")
     ap.add_argument("--procrustes", action="store_true", help="cfg4 sweep with Protocol #2 alignment")
     ap.add_argument("--no-data", action="store_true", help="skip the H3.6M preprocessing sub-measurement")
+    ap.add_argument("--no-stress", action="store_true", help="skip the cfg5 bf16 sub-measurement (infer mode)")
+    ap.add_argument("--stress-steps", type=int, default=64, help="cfg5 batches of 1024 timed (infer mode)")
     ap.add_argument("--data-frames", type=int, default=390000)
     ap.add_argument("--data-reps", type=int, default=10)
     ap.add_argument("--traffic", type=float, default=None,
@@ -902,7 +939,7 @@ def main():
         raise SystemExit("bench.py: --gpus %d but the job has %s rank(s) (WORLD_SIZE)"
                          % (args.gpus, os.environ.get("WORLD_SIZE", "1")))
     rank, world, local = setup_dist()
-    train = single = sweep = api = data = None
+    train = single = sweep = api = data = stress = None
     chain = None
     if args.mode == "infer":
         value, dt, roof = bench_serve(args, rank, world)
@@ -950,6 +987,15 @@ def main():
                 data = bench_data(args, rank, world)
             except Exception as exc:
                 data = {"error": repr(exc)[:300]}
+        if not args.no_stress:   # cfg5 beside the headline (bf16 / fp32-accumulate stress config)
+            try:
+                sv, sdt, sroof, ssteps = bench_stress(args, rank, world, steps=args.stress_steps, warmup=32)
+                stress = {"workload": "cfg5 inference: L=4096, 4 residual blocks, BN(eval), batch 1024 per step, "
+                                      "bf16 weights/activations, fp32 accumulate", "value": round(sv, 1),
+                          "unit": "poses/s", "steps": ssteps, "ms_per_step": round(1000.0 * sdt / ssteps, 5),
+                          "dtype": "bf16", "roofline": sroof}
+            except Exception as exc:
+                stress = {"error": repr(exc)[:300]}
     elif args.mode == "eval":
         sweep = bench_eval(args, rank, world)
         value, dt, roof = sweep["value"], sweep["ms_per_sweep"] / 1000.0, sweep.pop("roofline")
@@ -1003,6 +1049,8 @@ def main():
             line["api_step"] = api
         if data is not None and args.mode != "data":
             line["data_pipeline"] = data
+        if stress is not None:
+            line["stress"] = stress
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -87,7 +87,10 @@ int p3d_flat_ptr(p3d_model* m, int32_t which /*0 params,1 grads,2 adam_m,3 adam_
 int p3d_params_updated(p3d_model* m, void* stream);
 
 /* Forward pass: y[B, output_size] = MLP(x[B, input_size]).
- *   training=0: BN uses moving statistics (isTraining=False, linear_model.py:239-245)
+ *   training=0: BN uses moving statistics (isTraining=False, linear_model.py:239-245);
+ *               at B <= 4 (env P3D_GEMV_MAXB) every layer is a weight-streaming GEMV kernel
+ *               (the per-frame step of src/openpose_3dpose_sandbox.py:353-356); results
+ *               equal the MFMA path's to fp32 rounding, rows independent of B.
  *   training=1: BN uses batch statistics, updates the moving averages
  *               (UPDATE_OPS, linear_model.py:138-140) and caches activations
  *               for p3d_backward.  Requires B <= max_batch.
@@ -118,6 +121,12 @@ int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t tr
 int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
 /* 0 if every p3d_serve launch so far completed its synchronisation (device read; syncs). */
 int p3d_serve_check(p3d_model* m);
+
+/* 0 if every BN-train exchange so far completed (device read; syncs).  Training layers with
+ * batch norm run as one launch each whose row-tile workgroups swap their column statistics
+ * inside the launch; a spin that ran out (workgroups not co-resident, e.g.
+ * another persistent kernel holding CUs) sets a word this reports once, as P3D_ERR_HIP. */
+int p3d_sync_check(p3d_model* m);
 
 /* MSE loss of linear_model.py:129 and its gradient: loss = mean((y-t)^2) over
  * B*D, dy = (1/(B*D)) * 2*(y-t).  loss_dev: one device float (may be NULL),
@@ -200,7 +209,8 @@ int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const 
 
 /* rocprofv3 name of the kernel used for `what` under the model's tiling variants:
  * 0 = inference hidden layer at B <= 64, 1 = inference hidden layer at large M,
- * 2 = BN-train hidden-layer GEMM.  (Measurement plumbing for bench.py.) */
+ * 2 = BN-train hidden-layer GEMM, 3 = the kernel of the last p3d_serve launch,
+ * 4 = inference hidden layer at B <= 4 (weight-streaming GEMV).  (Measurement plumbing for bench.py.) */
 int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len);
 
 /* Host-binding plumbing: a DLPack v0.8 DLManagedTensor aliasing `data` (no copy; the

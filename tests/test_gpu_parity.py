@@ -90,6 +90,46 @@ def test_eval_forward_large_batch(B, residual, batch_norm, max_norm, keep):
     m.close()
 
 
+@pytest.mark.parametrize("L,N,B,residual,batch_norm,max_norm,keep,p14", [
+    (1024, 2, 1, True, True, False, 1.0, False), (1024, 2, 2, True, True, False, 1.0, False),
+    (1024, 2, 3, True, True, True, 1.0, False), (1024, 2, 4, True, True, False, 0.5, False),
+    (256, 3, 1, False, True, False, 1.0, False), (256, 1, 4, True, False, False, 1.0, True),
+    (2048, 1, 2, True, True, False, 1.0, False)])
+def test_gemv_small_batch(L, N, B, residual, batch_norm, max_norm, keep, p14, monkeypatch):
+    """Batch <= 4 inference through the weight-streaming k_gemv layers (the per-frame call of
+    src/openpose_3dpose_sandbox.py:353-356) vs the fp64 oracle; rows independent (every row
+    bit-identical to its own batch-1 call, also from another workspace row); agreement with
+    the 16-row MFMA kernels (P3D_GEMV_MAXB=0) within the same tolerance."""
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
+                      predict_14=p14)
+    st, m = make(cfg, batch=B, max_batch=64)
+    rng = np.random.default_rng(100 + B)
+    x = rng.standard_normal((B, 32)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    import ctypes
+    import _p3d
+    _p3d.check(_p3d.lib().p3d_profile_start(m._h, 64), "p3d_profile_start")
+    y = m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy()
+    buf = ctypes.create_string_buffer(1 << 12)
+    _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
+    tags = {ln.split("\t")[0]: int(ln.split("\t")[1]) for ln in buf.value.decode().strip().splitlines()}
+    assert tags == {"gemv_in": 1, "gemv_hidden": 2 * N, "gemv_out": 1}, tags
+    ro, _ = ref_mlp.forward(st, x, False, keep, m.seed, 3, 8)
+    close(y, ro)
+    for r in range(B):
+        y1 = m.forward_device(xd[r:r + 1].contiguous(), False, keep, ctr=3, row_offset=8 + r).cpu().numpy()
+        np.testing.assert_array_equal(y1[0], y[r])
+    y16 = torch.empty((B, m.output_size), dtype=torch.float32, device="cuda")
+    m.forward_device(xd, False, keep, ctr=3, row_offset=8, out=y16, ws_row=16)
+    np.testing.assert_array_equal(y16.cpu().numpy(), y)
+    m.close()
+    monkeypatch.setenv("P3D_GEMV_MAXB", "0")
+    st, m = make(cfg, batch=B, max_batch=64)
+    ym = m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy()
+    close(ym, y, atol=4e-5, rtol=4e-5)
+    m.close()
+
+
 @pytest.mark.parametrize("B,keep,max_norm", [(64, 1.0, False), (37, 0.5, False), (64, 1.0, True)])
 def test_transposed_inference_kernels_bit_identical(B, keep, max_norm, monkeypatch):
     """k_fwd_t (transposed accumulator, float4 epilogue) == k_fwd, bit for bit."""
@@ -145,11 +185,13 @@ def test_gradients_variants(residual, batch_norm, max_norm, B):
                             max_norm=max_norm), 0.5, B)
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
-def test_train_steps_track_oracle(split, monkeypatch):
-    """5 TF1 train steps vs the oracle.  split=1: BN-train layers as 16x16-tile GEMM +
-    k_bn_fwd / k_bn_bwd (default); split=0: whole-batch-per-workgroup kernels."""
+@pytest.mark.parametrize("split,xchg", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_train_steps_track_oracle(split, xchg, monkeypatch):
+    """5 TF1 train steps vs the oracle.  split=1: BN-train layers as 16x16-tile GEMMs, each
+    ONE launch whose row-tile workgroups exchange their column statistics (xchg=1, default)
+    or followed by k_bn_fwd / k_bn_bwd (xchg=0); split=0: whole-batch-per-workgroup kernels."""
     monkeypatch.setenv("P3D_TRAIN_SPLIT", split)
+    monkeypatch.setenv("P3D_TRAIN_XCHG", xchg)
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     st, m = make(cfg, lr=1e-3)
     rng = np.random.default_rng(21)
@@ -171,6 +213,50 @@ def test_train_steps_track_oracle(split, monkeypatch):
         err = np.abs(w[name] - st.params[name]).max()
         assert err < 5e-5, (name, err)
     m.close()
+
+
+@pytest.mark.parametrize("L,B,keep", [(1024, 64, 0.5), (256, 17, 0.5), (256, 64, 1.0), (256, 200, 0.5)])
+def test_bn_exchange_bit_identical_to_split(L, B, keep, monkeypatch):
+    """BN-train layers as ONE launch (row-tile workgroups swap their column statistics in the
+    launch, p3d_xchg.h) == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit, over 4
+    fused train steps: outputs, loss, weights, Adam slots, moving statistics.  B = 200 (13 row
+    tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4."""
+    import ctypes
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=2, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=6, bn_seed=7)
+    ms = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("P3D_TRAIN_XCHG", flag)
+        m = linear_model.LinearModel(L, 2, True, True, False, B, 1e-3, "/tmp/p3d_test", seed=9, max_batch=max(B, 64))
+        m.set_weights({**st.params, **st.moving})
+        ms.append(m)
+    xm, sm = ms
+    rng = np.random.default_rng(L + B)
+    for step in range(4):
+        x = torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)).cuda()
+        t = torch.from_numpy(rng.standard_normal((B, 48)).astype(np.float32)).cuda()
+        ys = []
+        for m in ms:
+            if step == 3:
+                _p3d.check(_p3d.lib().p3d_profile_start(m._h, 256), "p3d_profile_start")
+            ys.append(m.train_step_device(x, t, keep, out=torch.empty((B, 48), device="cuda"))[1])
+            if step == 3:
+                buf = ctypes.create_string_buffer(1 << 14)
+                _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
+                m.tags = {ln.split("\t")[0] for ln in buf.value.decode().strip().splitlines()}
+        assert torch.equal(ys[0], ys[1]), step
+        assert torch.equal(xm._loss_dev, sm._loss_dev), step
+    xm.sync_check()
+    for k in ("params", "moving", "adam_m", "adam_v"):
+        if xm.flat[k] is not None:
+            assert torch.equal(xm.flat[k], sm.flat[k]), k
+    assert xm.get_step() == sm.get_step()
+    # the exchange form really ran: no second BN launch in either direction
+    assert "fwd_hidden_train_x" in xm.tags and not {"bn_fwd", "bn_bwd"} & xm.tags, xm.tags
+    assert {"bn_fwd", "bn_bwd"} <= sm.tags, sm.tags
+    xm.close()
+    sm.close()
 
 
 @pytest.mark.parametrize("B", [128, 200])
@@ -392,8 +478,10 @@ def test_bad_shapes_raise():
 @pytest.mark.parametrize("L,N,B", [(256, 2, 128), (512, 1, 200), (4096, 4, 1024)])
 def test_bf16_inference_matches_emulated_oracle(L, N, B):
     """cfg5 path (bf16 weights/activations, fp32 accumulate) vs the oracle's bf16 emulation.
-    Tolerance: 2% of the output range (one bf16 ulp is 0.4%; a flipped rounding of a hidden
-    activation propagates), and 2e-3 mean absolute deviation."""
+    Tolerances, relative to the output range, from the measured distribution (tools/bf16_err_probe.py
+    on MI355X, 3 seeds per shape; a flipped bf16 rounding of a hidden activation propagates, and at
+    L = 4096 the oracle accumulates in fp32 in another order): L = 4096 max 3.9e-3 / mean 3.4e-4
+    -> 1e-2 / 1e-3; L <= 512 max 3.5e-4 / mean 1.0e-6 -> 1e-3 / 1e-5."""
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
     st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
     m = linear_model.LinearModel(L, N, True, True, False, B, 1e-3, "/tmp/p3d_test", dtype="bfloat16",
@@ -404,8 +492,9 @@ def test_bf16_inference_matches_emulated_oracle(L, N, B):
     ref = ref_mlp.forward_bf16(st, x, acc=np.float32 if L >= 4096 else np.float64)
     scale = np.abs(ref).max()
     err = np.abs(y - ref)
-    assert err.max() <= 0.02 * scale, (err.max(), scale)
-    assert err.mean() <= 2e-3 * scale, (err.mean(), scale)
+    tmax, tmean = (1e-2, 1e-3) if L >= 4096 else (1e-3, 1e-5)
+    assert err.max() <= tmax * scale, (err.max(), scale)
+    assert err.mean() <= tmean * scale, (err.mean(), scale)
     # and it is close to the fp32 model (bf16 is an approximation of cfg2's arithmetic)
     ref32, _ = ref_mlp.forward(st, x, False)
     assert np.abs(y - ref32).mean() <= 0.05 * np.abs(ref32).mean()
