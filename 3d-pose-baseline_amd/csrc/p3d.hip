@@ -1316,7 +1316,8 @@ struct p3d_model {
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
   int serve6 = 1;           // k_serve6 for launches of <= serve6_max_nb steps (env P3D_SERVE6: 0 off, 1 auto, 2 always)
   int serve6_max_nb = 32;   // (env P3D_SERVE6_MAX_NB)
-  int serve6_split = 0;     // k_serve6 groups per XCD, 0 = chosen per launch (env P3D_SERVE6_SPLIT: 1..4)
+  int serve6_split = 0;     // k_serve6 groups per XCD, 0 = chosen per launch (env P3D_SERVE6_SPLIT: 1..8)
+  int serve6_rt = 0;        // k_serve6 row tiles per unit, 0 = chosen per launch (env P3D_SERVE6_RT: 4 or 2)
   int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
   std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
@@ -1607,6 +1608,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_SERVE6")) m->serve6 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_MAX_NB")) m->serve6_max_nb = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_SPLIT")) m->serve6_split = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6_RT")) m->serve6_rt = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_DEPTH")) m->serve6_depth = atoi(ev);
   {
     StepState s0{};
@@ -2188,41 +2190,51 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
 // (hand-off, ring fill, K-combine, epilogue) ~4 us, a column tile of K = 1024 ~3.9 us
 // (round-1 phase traces).  nb = 20 -> S = 3 (all steps at once, <= 7 tiles per
 // CU); nb <= 8 -> S = 1; nb = 16 -> S = 2.
-static int serve6_ncm(const p3d_model* m, int S, int T);
-// tiles a member of the smallest group holds, and whether the form built for it covers them
-// (a member keeps the epilogue constants of at most ECT tiles in LDS, p3d_serve6.h)
-static bool serve6_fits(const p3d_model* m, int S, int T) {
-  const int nmin = std::max(1, m->serve_grid / 8) / S;
-  if (nmin < 1) return false;
-  const int need = (T + nmin - 1) / nmin, ncm = serve6_ncm(m, S, T);
-  return need <= (ncm >= 7 ? ncm : 2 * ncm);
+// A k_serve6 launch shape: S groups per XCD, RT row tiles per unit (4: batch-64 steps, 2:
+// 32-row half steps), NCM column tiles per contraction (the built form covering a member of the
+// smallest group; its epilogue constants of at most ECT tiles sit in LDS, p3d_serve6.h).
+struct Serve6Plan { int S = 0, rt = 4, ncm = 0; };
+
+static int serve6_ncm_for(int rt, int need) {
+  if (rt == 2) return need <= 11 ? 11 : 0;
+  return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : need <= 8 ? 8 : 0;
 }
 
-static int serve6_split_for(const p3d_model* m, int64_t nb, int T) {
-  if (m->serve6_split >= 1 && m->serve6_split <= 4) return serve6_fits(m, m->serve6_split, T) ? m->serve6_split : 0;
+// The plan minimising (rounds of units) x (fixed cost per phase + cost per column tile x tiles
+// per CU), 32 CUs per XCD (grid / 8): a phase's fixed cost (hand-off, ring fill, K-combine,
+// epilogue) ~4 us, a column tile of K = 1024 ~3.9 us at 4 row tiles (round-1 phase traces,
+// DESIGN.md 5a) and ~0.55 of that at 2 (the weight fragments serve half the rows).  B rows:
+// 20 batch-64 steps (1280 rows) -> RT = 2, S = 5: 40 units on 40 groups of 6-7 CUs, <= 11 tiles
+// each; 8 steps -> RT = 4, S = 1; 16 -> RT = 4, S = 2.
+static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
   const int cx = std::max(1, m->serve_grid / 8);
-  const double cfix = 4.0, ctile = 3.9 * T / 64.0;
-  int best = 0;
+  const double cfix = 4.0;
+  Serve6Plan best;
   double bt = 1e30;
-  for (int S = 1; S <= 4; ++S) {
-    const int nmin = cx / S;
-    if (nmin < 1 || !serve6_fits(m, S, T)) continue;
-    const double rounds = (double)((nb + 8 * S - 1) / (8 * S));
-    const double t = rounds * (cfix + ctile * ((T + nmin - 1) / nmin));
-    if (t < bt - 1e-9) { bt = t; best = S; }
+  for (int rt = 4; rt >= 2; rt -= 2) {
+    if (m->serve6_rt && m->serve6_rt != rt) continue;
+    const int64_t nb = (B + 16 * rt - 1) / (16 * rt);
+    const double ctile = (rt == 4 ? 3.9 : 0.55 * 3.9) * T / 64.0;
+    for (int S = 1; S <= (rt == 4 ? 4 : 8); ++S) {
+      if (m->serve6_split && m->serve6_split != S) continue;
+      const int nmin = cx / S;
+      if (nmin < 1) continue;
+      const int need = (T + nmin - 1) / nmin, ncm = serve6_ncm_for(rt, need);
+      if (!ncm || need > (ncm >= 7 ? ncm : 2 * ncm)) continue;
+      const double rounds = (double)((nb + 8 * S - 1) / (8 * S));
+      const double t = rounds * (cfix + ctile * need);
+      if (t < bt - 1e-9) { bt = t; best.S = S; best.rt = rt; best.ncm = ncm; }
+    }
   }
   return best;
 }
 
-// column tiles per contraction: the smallest built form covering a member of the smallest group
-static int serve6_ncm(const p3d_model* m, int S, int T) {
-  const int nmin = std::max(1, std::max(1, m->serve_grid / 8) / S);
-  const int need = (T + nmin - 1) / nmin;
-  return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : 8;
-}
-
-static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, unsigned grid, hipStream_t st,
-                          const ServeArgs& a) {
+static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, int rt, unsigned grid,
+                          hipStream_t st, const ServeArgs& a) {
+  if (rt == 2) {   // 32-row units, 11 column tiles (S = 5)
+    go(ps, k_serve6<2, 3, 11, 2>, dim3(grid), dim3(256), st, a);
+    return;
+  }
   // ring depth 4 for the narrow forms; 2 for 7 / 8 tiles (depth 4 spills there: 77 / 136
   // registers; depth 2 none / 38)
   if (ncm == 2) {
@@ -2274,7 +2286,7 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     m->serve_err = (int*)(m->serve_sync + 2 * P3D_SERVE_SYNC_WORDS);
   }
   ServeArgs a{};
-  a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);
+  a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);   // batch-64 steps (k_serve6 may halve them)
   a.L = L; a.K0 = c.input_size; a.ND = c.output_size; a.nblk = c.num_layers;
   a.bn = c.batch_norm; a.residual = c.residual; a.eps = c.bn_eps;
   a.act = m->serve_buf; a.part = m->serve_buf + P3D_SERVE_GROUPS * 3 * slab;
@@ -2291,9 +2303,12 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     s.wsq = c.max_norm ? m->wsq + ly.widx : nullptr;
   }
   bool use6 = m->serve6 && c.num_layers > 0 && NDT == 3 && (m->serve6 == 2 || a.nb <= (int64_t)m->serve6_max_nb);
+  Serve6Plan plan;
   if (use6) {
-    a.split = serve6_split_for(m, a.nb, L / 16);
-    use6 = a.split > 0;                      // no form covers this width: k_serve5
+    plan = serve6_plan(m, B, L / 16);
+    a.split = plan.S;
+    use6 = plan.S > 0;                       // no form covers this width: k_serve5
+    if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
   }
   if (use6) {
     // no memset in front: this launch's bank was zeroed by the previous k_serve6 launch (or at
@@ -2313,11 +2328,12 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   }
   if (use6) {
     const int T = L / 16;
-    const int ncm = serve6_ncm(m, a.split, T);
-    const int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
-    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ">";
+    const int ncm = plan.ncm;
+    const int depth = plan.rt == 2 ? 2 : ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
+    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) +
+                     (plan.rt == 2 ? ", 2>" : ", 4>");
     ProfScope ps(m, "serve");
-    launch_serve6(ps, m, ncm, depth, (unsigned)m->serve_grid, st, a);
+    launch_serve6(ps, m, ncm, depth, plan.rt, (unsigned)m->serve_grid, st, a);
   } else {
     m->serve_kname.clear();
     ProfScope ps(m, "serve");

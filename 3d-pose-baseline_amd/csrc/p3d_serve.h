@@ -58,7 +58,7 @@
 // serialised 256 atomics, ~9.6 us per launch), [P3D_SERVE_FLAG0 + 64 g + r] flag of member r
 // of group g
 #define P3D_SERVE_FLAG0 256
-#define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 32)
+#define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 64)   // flags of up to 64 groups (k_serve6 S <= 8)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads

@@ -46,23 +46,6 @@
 #define P3D_S6_STAMP(row, k) do { } while (0)
 #endif
 
-// Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
-// rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
-// [0] start, [1] census, [2] input layer, [3] first hand-off; per hidden phase ph at 8 ph:
-// [0] begin, [1] contraction, [2] K-combine, [3] epilogue, [4] hand-off; at 8 (NH + 1): [0]
-// the output reduction.  wall_clock64 (100 MHz).
-#ifdef P3D_TRACE
-#define P3D_S6_STAMP(row, k)                                                              \
-  do {                                                                                    \
-    if (tr6 && (row) && threadIdx.x == 0) {                                               \
-      tr6[(k)] = wall_clock64();                                                          \
-      tr6[64 + (k)] = __builtin_amdgcn_s_memtime();                                       \
-    }                                                                                     \
-  } while (0)
-#else
-#define P3D_S6_STAMP(row, k) do { } while (0)
-#endif
-
 // The serve launch's prologue kernel (in place of a memset of the sync words, so no extra
 // launch): zero the sync words and form the epilogue constants of every layer 0..2N and
 // column -- bias, inv = gamma / sqrt(var + eps), shift = beta - mean * inv, the arithmetic of
@@ -90,18 +73,24 @@ __global__ __launch_bounds__(256) void k_serve_prep(ServeArgs p, float* ecg) {
 // owner of column tile t when T tiles are dealt contiguously over n members
 __device__ __forceinline__ int p3d_tile_owner(int t, int n, int T) { return ((t + 1) * n - 1) / T; }
 
-template <int DEPTH, int NDT, int NCM>
+// RT: row tiles per step unit (4: the batch-64 step; 2: half a step, 32 rows -- rows are
+// independent in evaluation, so a launch of nb batch-64 steps may run as 2 nb units of 32 rows:
+// 20 steps = 40 units = 5 groups on each of the 8 XCDs, no group idle; p3d.hip serve6_plan)
+template <int DEPTH, int NDT, int NCM, int RT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve6(ServeArgs p) {
+  static_assert(RT == 4 || RT == 2, "row tiles per unit");
   constexpr int RE = P3D_SERVE6_RE;
-  constexpr int PT = 4 * NDT * 256;          // floats of one tile's output partial
-  constexpr int E4 = 4 * NDT * 64;           // float4 elements of a step's output
+  constexpr int ROWS = 16 * RT;              // rows of one unit
+  constexpr int WPR = 4 / RT;                // waves per row tile in the epilogue / input layer
+  constexpr int PT = RT * NDT * 256;         // floats of one tile's output partial
+  constexpr int E4 = RT * NDT * 64;          // float4 elements of a unit's output
   constexpr int DA = NCM >= 7 && DEPTH > 2 ? 2 : DEPTH;   // activation ring depth
 #ifndef P3D_S6_PD
   constexpr int PD = NCM <= 4 ? 2 : 1;       // ring slots prefetched off-contraction
 #else
   constexpr int PD = P3D_S6_PD;
 #endif
-  __shared__ __attribute__((aligned(16))) f32x4 red[4 * 4 * NCM * 64];   // [slice][rt][tile][lane]
+  __shared__ __attribute__((aligned(16))) f32x4 red[4 * RT * NCM * 64];  // [slice][rt][tile][lane]
   __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64 * RE];       // split output reduction
   // epilogue constants of the member's tiles (up to ECT of them), per layer 0..2N:
   // bias | inv | shift, and each layer's max-norm divisor.  Every epilogue reads them from
@@ -118,6 +107,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
   const int q4 = 4 * (lane >> 4);
   const int S = p.split;
+  // the row tile this wave finishes, and which of the chunk's tiles (cc % WPR == csel)
+  const int rtw = w % RT, csel = w / RT;
 #ifdef P3D_TRACE
   const unsigned long long t_start = wall_clock64();
   unsigned long long* tr6 = nullptr;
@@ -131,7 +122,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     unsigned* other = p.sync_next;
     for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
   }
-  p3d_serve_census(p, sh, (S < 1 || S > 4) ? -1 : 64 * S);
+  p3d_serve_census(p, sh, (S < 1 || S > 8) ? -1 : 64 * S);
   if (!sh[2]) {
   const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
   const int nx = __builtin_amdgcn_readfirstlane(sh[8 + xcc]);
@@ -156,7 +147,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     gi = p.nb;                               // the whole group reports instead of computing
   }
   unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;   // (p.sync: this launch's bank)
-  const int64_t slab = (int64_t)64 * L;
+  const int64_t slab = (int64_t)ROWS * L;
   float* act = p.act + (int64_t)gid * 3 * slab;
   float* part = p.part + (int64_t)gid * 2 * T * PT;
   const ServeLayer& li = p.ly[0];
@@ -181,7 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool split_red = t_lo < t_hi && ecnt <= 64 * RE;
 
   auto in_issue = [&](int64_t rbase, int c0, f32x4 (&xa)[4], f32x4 (&wb)[NCM][4]) {
-    int64_t rowc = rbase + 16 * w + (lane & 15);
+    int64_t rowc = rbase + 16 * rtw + (lane & 15);
     rowc = rowc < p.M ? rowc : p.M - 1;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -198,7 +189,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the group's first step's input-layer operands, requested before the epilogue constants
   // are copied (their latencies overlap)
   f32x4 xa0[4], wb0[NCM][4];
-  if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * 64, t_lo, xa0, wb0);
+  if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * ROWS, t_lo, xa0, wb0);
   {   // epilogue constants of this member's tiles, formed once per launch: bias, inv = gamma /
       // sqrt(var + eps), shift = beta - mean * inv (the arithmetic of every other path), and
       // each layer's max-norm divisor.  Every thread's operand loads are issued before the
@@ -289,7 +280,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int nck = min(NCM, t_hi - c0);
 #pragma unroll
     for (int cc = 0; cc < NCM; ++cc) {
-      if (cc >= nck) continue;
+      if (cc >= nck || cc % WPR != csel) continue;
       const int t = c0 + cc;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -299,7 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[cc][g][e], xa[g][e], acc, 0, 0, 0);
       if (wsq_any) maxnorm_div(0, acc);
       const f32x4 y = epi_t(0, t - t_lo, acc);
-      *(f32x4*)(act + cbuf * slab + ((int64_t)(w * ngL + t) * 64 + lane) * 4) = y;
+      *(f32x4*)(act + cbuf * slab + ((int64_t)(rtw * ngL + t) * 64 + lane) * 4) = y;
     }
   };
   auto in_layer = [&](int64_t rbase, int cbuf, int cfrom) {
@@ -378,14 +369,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int64_t prev_row0 = -1;
   if (gi < p.nb) {                           // the group's first step: its input layer alone
     if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, 0);
-    in_layer((int64_t)gi * 64, 0, t_lo + NCM);
+    in_layer((int64_t)gi * ROWS, 0, t_lo + NCM);
     P3D_S6_STAMP(trs, 2);
     if (t_lo < t_hi) b_prefetch(1, t_lo);
     group_sync(false);
     P3D_S6_STAMP(trs, 3);
   }
   for (int b = gi; b < p.nb; b += ng, ++jl) {
-    const int64_t row0 = (int64_t)b * 64;
+    const int64_t row0 = (int64_t)b * ROWS;
     const bool has_next = b + ng < p.nb;
     const int c0n = (c0b + 2 * p.nblk) % 3;  // buffer the next step's input layer writes
     int cur = c0b;
@@ -429,7 +420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // register ring: weight fragments DEPTH k-groups ahead, activations DA ahead (the
         // weights stream from MALL/HBM, the activations are L2 hits; the wide forms cannot hold
         // both DEPTH deep: 4 x 11 fragments spilled 77 registers at NCM = 7)
-        f32x4 ra_[DA][4], rb_[DEPTH][NCM];
+        f32x4 ra_[DA][RT], rb_[DEPTH][NCM];
         // the first PD weight slots were requested off the previous contraction (b_prefetch
         // runs before every contraction); a compile-time split keeps the number of loads in
         // flight static, so the compiler's vmcnt waits stay exact
@@ -437,22 +428,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int d = 0; d < DEPTH; ++d) {
           if (d < DA)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+            for (int t = 0; t < RT; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
 #pragma unroll
           for (int cc = 0; cc < NCM; ++cc) rb_[d][cc] = d < PD ? rbp[d < PD ? d : 0][cc] : ldb(cc, d);
         }
-        f32x4 acc[NCM][4];
+        f32x4 acc[NCM][RT];
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc[cc][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int t = 0; t < RT; ++t) acc[cc][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         auto mfmas = [&](int d) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int cc = 0; cc < NCM; ++cc)
 #pragma unroll
-              for (int t = 0; t < 4; ++t)
+              for (int t = 0; t < RT; ++t)
                 acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d % DA][t][e], acc[cc][t], 0, 0, 0);
         };
         for (int g0 = 0; g0 < gcount - DEPTH; g0 += DEPTH) {
@@ -461,7 +452,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             mfmas(d);
             const int ga = g0 + d + DA, gn = g0 + DEPTH + d;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
+            for (int t = 0; t < RT; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
 #pragma unroll
             for (int cc = 0; cc < NCM; ++cc) rb_[d][cc] = ldb(cc, gn);
             __builtin_amdgcn_sched_barrier(0);   // refill of slot d stays ahead of slot d+1's MFMAs
@@ -473,7 +464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if (d + DA < DEPTH) {
             const int ga = gcount - DEPTH + d + DA;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
+            for (int t = 0; t < RT; ++t) ra_[d % DA][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + ga * 1024);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -490,7 +481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc) {
           const int t = c0 + (cc < nck ? cc : nck - 1);
-          rv[cc] = p3d_ld_sc1(rr, (int)(((int64_t)(w * ngL + t) * 64 + lane) * 16));
+          rv[cc] = p3d_ld_sc1(rr, (int)(((int64_t)(rtw * ngL + t) * 64 + lane) * 16));
           p3d_wo_load<NDT>(lo, t, ngL, wo[cc]);
         }
         // the next contraction's first weight slots: this member's next chunk, the next
@@ -505,22 +496,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) red[((w * 4 + t) * NCM + cc) * 64 + lane] = acc[cc][t];
+          for (int t = 0; t < RT; ++t) red[((w * RT + t) * NCM + cc) * 64 + lane] = acc[cc][t];
         __syncthreads();
         P3D_S6_STAMP(trs && first_c, 8 * ph + 2);
         f32x4 sacc[NCM];                       // K slices summed in slice order
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc) {
-          sacc[cc] = red[((0 * 4 + w) * NCM + cc) * 64 + lane];   // slice 0, tile (w, cc)
+          if (cc % WPR != csel) { sacc[cc] = f32x4{0.f, 0.f, 0.f, 0.f}; continue; }
+          sacc[cc] = red[((0 * RT + rtw) * NCM + cc) * 64 + lane];   // slice 0, tile (rtw, cc)
 #pragma unroll
-          for (int k = 1; k < 4; ++k) sacc[cc] += red[((k * 4 + w) * NCM + cc) * 64 + lane];
+          for (int k = 1; k < 4; ++k) sacc[cc] += red[((k * RT + rtw) * NCM + cc) * 64 + lane];
         }
         if (wsq_any)
 #pragma unroll
           for (int cc = 0; cc < NCM; ++cc) maxnorm_div(ph, sacc[cc]);
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc) {
-          if (cc >= nck) continue;
+          if (cc >= nck || cc % WPR != csel) continue;
           const int t = c0 + cc;
           f32x4 yv = epi_t(ph, t - t_lo, sacc[cc]);
           if (res) yv += rv[cc];
@@ -530,17 +522,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
               f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
               for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[cc][o][e], pacc, 0, 0, 0);
-              *(f32x4*)(pdst + (int64_t)t * PT + ((w * NDT + o) * 64 + lane) * 4) = pacc;
+              *(f32x4*)(pdst + (int64_t)t * PT + ((rtw * NDT + o) * 64 + lane) * 4) = pacc;
             }
           } else {
-            *(f32x4*)(Y + ((int64_t)(w * ngL + t) * 64 + lane) * 4) = yv;
+            *(f32x4*)(Y + ((int64_t)(rtw * ngL + t) * 64 + lane) * 4) = yv;
           }
         }
         // red / rsum are rewritten by this member's next contraction of the phase
         if (c0 + NCM < t_hi) __syncthreads();
       }
       // the next step's input layer (it depends on nothing of this step) in the last phase
-      if (lastp && has_next) in_layer(row0 + (int64_t)ng * 64, c0n, t_lo);
+      if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, c0n, t_lo);
       P3D_S6_STAMP(trs, 8 * ph + 3);
       if (second) cur = t2;
       // after a step's last phase the output reduction reads every tile's partial: the split

@@ -142,43 +142,48 @@ def test_serve_knob_variants_vs_oracle(monkeypatch, split, upm, depth, L, N):
     m.close()
 
 
-def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1):
+def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1, rt=None):
     if split is not None:
         monkeypatch.setenv("P3D_SERVE6_SPLIT", str(split))
     if mode is not None:
         monkeypatch.setenv("P3D_SERVE6", str(mode))
+    if rt is not None:
+        monkeypatch.setenv("P3D_SERVE6_RT", str(rt))
     st, m = make(cfg, seed=seed)
-    monkeypatch.delenv("P3D_SERVE6_SPLIT", raising=False)
-    monkeypatch.delenv("P3D_SERVE6", raising=False)
+    for k in ("P3D_SERVE6_SPLIT", "P3D_SERVE6", "P3D_SERVE6_RT"):
+        monkeypatch.delenv(k, raising=False)
     return st, m
 
 
 def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
-    """k_serve6 (launches of <= 32 steps; the driver's 20-step headline): 1, 2, 3 or 4 groups
-    per XCD (16-column tiles dealt contiguously, 7 tiles per CU at 3 groups) give the same bits --
-    the association of every sum is fixed by the tile, not by the group shape -- and the
-    oracle's outputs; the auto choice for 20 steps is the 3-group form."""
+    """k_serve6 (launches of <= 32 steps; the driver's 20-step headline): 1-4 groups per XCD of
+    batch-64 units (16-column tiles dealt contiguously, 7 tiles per CU at 3 groups) and 32-row
+    half-step units at 5 (and 3) groups per XCD give the same bits -- the association of every
+    sum is fixed by the tile, not by the group or unit shape -- and the oracle's outputs; the
+    auto choice for 20 steps is 40 half-step units on 5 groups per XCD (no group idle)."""
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     B = 64 * 20
     x = np.random.default_rng(620).standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
     outs = {}
-    for split in (None, 1, 2, 3, 4):
-        st, m = _serve6_model(monkeypatch, cfg, split)
+    for split, rt in ((None, None), (1, 4), (2, 4), (3, 4), (4, 4), (5, 2), (3, 2)):
+        st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
         y = m.serve_device(xd)
         torch.cuda.synchronize()
         m.serve_check()
         name = _p3d.ctypes.create_string_buffer(128)
         _p3d.check(_p3d.lib().p3d_kernel_name(m._h, 3, name, 128), "p3d_kernel_name")
         assert name.value.decode().startswith("k_serve6<"), name.value
-        outs[split] = (y, name.value.decode())
+        outs[(split, rt)] = (y, name.value.decode())
         m.close()
-    assert outs[None][1] == "k_serve6<2, 3, 7>", outs[None][1]     # nb = 20 -> 3 groups per XCD
-    for split in (1, 2, 3, 4):
-        assert torch.equal(outs[split][0], outs[None][0]), split
+    auto = outs[(None, None)]
+    assert auto[1] == "k_serve6<2, 3, 11, 2>", auto[1]     # 20 steps -> 40 half steps, 5 groups per XCD
+    assert outs[(3, 4)][1] == "k_serve6<2, 3, 7, 4>", outs[(3, 4)][1]
+    for key, (y, _) in outs.items():
+        assert torch.equal(y, auto[0]), key
     ro, _ = ref_mlp.forward(st, x, False, 1.0, 0, 0, 0)
-    close(outs[None][0].cpu().numpy(), ro)
+    close(auto[0].cpu().numpy(), ro)
 
 
 @pytest.mark.parametrize("B", [1, 13, 64, 64 * 5 + 7, 64 * 8, 64 * 16, 64 * 24 + 1, 64 * 32])
@@ -205,11 +210,11 @@ def test_serve6_launch_sizes_vs_oracle(B):
     (1024, 2, True, True, False, True),      # --predict_14
     (2048, 1, True, True, False, False),     # 128 tiles: 13 per CU at 3 groups -> two contractions
 ])
-@pytest.mark.parametrize("split", [None, 3])
-def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split):
+@pytest.mark.parametrize("split,rt", [(None, None), (3, 4), (5, 2)])
+def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split, rt):
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
                       predict_14=p14)
-    st, m = _serve6_model(monkeypatch, cfg, split)
+    st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
     B = 64 * 20 + 5
     x = np.random.default_rng(L + N).standard_normal((B, 32)).astype(np.float32)
     y = m.serve_device(torch.from_numpy(x).cuda()).cpu().numpy()
@@ -219,8 +224,8 @@ def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_
     m.close()
 
 
-@pytest.mark.parametrize("split", [1, 2, 3])
-def test_serve6_many_steps_per_group(monkeypatch, split):
+@pytest.mark.parametrize("split,rt", [(1, 4), (2, 4), (3, 4), (5, 2)])
+def test_serve6_many_steps_per_group(monkeypatch, split, rt):
     """k_serve6 forced on a long launch (P3D_SERVE6=2): every group runs many steps, so the
     next step's input layer rides in the last phase and each step's output is reduced in the
     next step's first phase (split over the members); every row vs the oracle / k_serve5."""
@@ -228,7 +233,7 @@ def test_serve6_many_steps_per_group(monkeypatch, split):
     B = 64 * 300 + 9
     x = np.random.default_rng(77 + split).standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
-    st, m6 = _serve6_model(monkeypatch, cfg, split, mode=2)
+    st, m6 = _serve6_model(monkeypatch, cfg, split, mode=2, rt=rt)
     y6 = m6.serve_device(xd)
     torch.cuda.synchronize()
     m6.serve_check()
