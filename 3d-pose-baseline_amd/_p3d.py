@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P3D_LIB", os.path.join(HERE, "libp3d.so"))  # P3D_LIB: dev builds (tools/)
@@ -81,6 +81,7 @@ SIGNATURES = [
                                   c_void_p, c_void_p]),
     ("p3d_moments_workspace", c_int64, [c_int64, c_int32]),
     ("p3d_moments", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    ("p3d_crc32c", c_uint32, [c_void_p, c_int64, c_uint32]),
 ]
 
 

@@ -96,6 +96,21 @@ def read_npy_dump(directory: str):
     return out
 
 
+def check_state(model, state):
+    """Reject variables this model does not have and shape mismatches (TF's restore raises
+    NotFoundError / InvalidArgumentError for both)."""
+    known = set(global_order(model.param_table))
+    unknown = sorted(set(state) - known)
+    if unknown:
+        raise ValueError("checkpoint variables not in this model: %s" % ", ".join(unknown[:8]))
+    shapes = model._shapes
+    for name, val in state.items():
+        want = shapes.get(name[:-len("/Adam_1")] if name.endswith("/Adam_1") else
+                          name[:-len("/Adam")] if name.endswith("/Adam") else name)
+        if want is not None and tuple(np.shape(val)) != tuple(want):
+            raise ValueError("%s: checkpoint shape %s, model shape %s" % (name, np.shape(val), tuple(want)))
+
+
 def import_npy_dump(model, directory: str):
     """Load a trainable or global npy dump into the model (unknown names are rejected)."""
     state = read_npy_dump(directory)

@@ -2990,3 +2990,46 @@ extern "C" int p3d_moments(const double* x, int64_t F, int32_t D, double* mean, 
   LAUNCH_CHECK("k_col_partial");
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78) of host memory, slicing-by-8: the
+// checksum of TF's tensor bundles (every tensor's bytes and every index-table block,
+// checkpoint_io.py / tf_bundle.py), far too slow byte by byte in Python for 51 MB of state.
+// crc = p3d_crc32c(data, n, 0) for a whole buffer; pass the previous result to continue.
+// ---------------------------------------------------------------------------------------
+namespace {
+struct Crc32cTables {
+  uint32_t t[8][256];
+  Crc32cTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFFu];
+  }
+};
+const Crc32cTables& crc32c_tables() {
+  static const Crc32cTables tb;
+  return tb;
+}
+}  // namespace
+
+extern "C" uint32_t p3d_crc32c(const void* data, int64_t n, uint32_t crc) {
+  const Crc32cTables& tb = crc32c_tables();
+  const unsigned char* p = (const unsigned char*)data;
+  uint32_t c = ~crc;
+  while (n > 0 && ((uintptr_t)p & 7)) { c = (c >> 8) ^ tb.t[0][(c ^ *p++) & 0xFFu]; --n; }
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    const uint32_t lo = (uint32_t)v ^ c, hi = (uint32_t)(v >> 32);
+    c = tb.t[7][lo & 0xFF] ^ tb.t[6][(lo >> 8) & 0xFF] ^ tb.t[5][(lo >> 16) & 0xFF] ^ tb.t[4][lo >> 24] ^
+        tb.t[3][hi & 0xFF] ^ tb.t[2][(hi >> 8) & 0xFF] ^ tb.t[1][(hi >> 16) & 0xFF] ^ tb.t[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n-- > 0) c = (c >> 8) ^ tb.t[0][(c ^ *p++) & 0xFFu];
+  return ~c;
+}

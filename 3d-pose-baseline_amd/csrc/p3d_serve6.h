@@ -168,9 +168,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) { tr6[0] = t_start; tr6[1] = wall_clock64(); }
   }
 #endif
-  bool trs = true;                           // stamping this step (the group's first)
   const bool split_red = t_lo < t_hi && ecnt <= 64 * RE;
 
+  bool trs = true;                           // stamping this step (the group's first)
   auto in_issue = [&](int64_t rbase, int c0, f32x4 (&xa)[4], f32x4 (&wb)[NCM][4]) {
     int64_t rowc = rbase + 16 * rtw + (lane & 15);
     rowc = rowc < p.M ? rowc : p.M - 1;
@@ -229,6 +229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tid < nl) ecm[tid] = wsq_any ? fmaxf(sqrtf(wq), 1.0f) : 1.0f;
     __syncthreads();
   }
+  P3D_S6_STAMP(trs, 4);
   // epilogue of tile t (chunk position cc) of layer l: z = acc / maxnorm + b, relu(z * inv + shift)
   // acc already divided by the max-norm divisor (maxnorm_div, a uniform branch of its own:
   // a per-element select made every epilogue run the division sequence)
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int64_t prev_row0 = -1;
   if (gi < p.nb) {                           // the group's first step: its input layer alone
     if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, 0);
+    P3D_S6_STAMP(trs, 5);
     in_layer((int64_t)gi * ROWS, 0, t_lo + NCM);
     P3D_S6_STAMP(trs, 2);
     if (t_lo < t_hi) b_prefetch(1, t_lo);

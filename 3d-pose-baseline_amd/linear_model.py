@@ -107,8 +107,14 @@ class Placeholder:
 
 
 class Saver:
-    """tf.train.Saver stand-in: every global variable (TF names), Adam slots and step
-    bookkeeping into ``<save_path>-<global_step>.npz``; keeps the last ``max_to_keep``."""
+    """tf.train.Saver (src/linear_model.py:151, max_to_keep=10): every global variable under
+    its TF name -- weights, BN moving statistics, learning_rate, global_step (int32, as the
+    reference's ``tf.Variable(0)``), beta1/2_power and the Adam slots -- into a TensorFlow V2
+    checkpoint ``<save_path>-<global_step>.index`` / ``.data-00000-of-00001`` plus the
+    ``checkpoint`` state file (tf_bundle.py), so the reference's ``--load`` check
+    (``checkpoint-N.index``, src/predict_3dpose.py:172) and TF itself can read what this
+    writes, and this restores checkpoints TF wrote.  ``.npz`` checkpoints of earlier builds
+    are still restored."""
 
     def __init__(self, model, max_to_keep=10):
         self.model = model
@@ -118,23 +124,23 @@ class Saver:
     def save(self, session, save_path, global_step=None):
         """Collective under data parallelism: every rank calls it (the moving statistics are
         averaged over the replicas), rank 0 alone writes, and the ranks leave together."""
+        import tf_bundle
         path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
         self.model.sync_moving_stats()   # data parallel: one set of moving statistics
         if self.model.rank != 0:
             self._barrier()
             return path
         state = self.model.get_state()
-        d = os.path.dirname(path)
-        if d:
-            os.makedirs(d, exist_ok=True)
-        np.savez(path + ".npz", **state)
-        with open(os.path.join(d or ".", "checkpoint"), "w") as f:
-            f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
-        self._saved.append(path)
+        state["global_step"] = np.asarray(state["global_step"], np.int32)
+        tf_bundle.write_bundle(path, state)
+        self._saved = [p for p in self._saved if p != path] + [path]
         while len(self._saved) > self.max_to_keep:
             old = self._saved.pop(0)
-            if os.path.exists(old + ".npz"):
-                os.remove(old + ".npz")
+            for f in (old + ".index", tf_bundle.data_path(old)):
+                if os.path.exists(f):
+                    os.remove(f)
+        d = os.path.dirname(path)
+        tf_bundle.write_checkpoint_state(d, os.path.basename(path), [os.path.basename(p) for p in self._saved])
         self._barrier()
         return path
 
@@ -154,6 +160,14 @@ class Saver:
         return checkpoint_io.import_npy_dump(self.model, directory)
 
     def restore(self, session, save_path):
+        """Restore a V2 checkpoint prefix (TF's or this build's), or an earlier build's .npz."""
+        import checkpoint_io
+        import tf_bundle
+        if os.path.isfile(save_path + ".index"):
+            state = tf_bundle.read_bundle(save_path)
+            checkpoint_io.check_state(self.model, state)
+            self.model.set_state(state)
+            return
         p = save_path if save_path.endswith(".npz") else save_path + ".npz"
         if not os.path.exists(p):
             raise ValueError("Checkpoint %s does not seem to exist" % save_path)

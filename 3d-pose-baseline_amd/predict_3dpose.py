@@ -132,8 +132,11 @@ def create_model(session, actions, batch_size, flags=None):
     if flags.load <= 0:
         print("Creating model with fresh parameters.")
         return model
+    import tf_bundle
+    if tf_bundle.read_checkpoint_state(tdir) is None and not os.path.isdir(tdir):
+        raise ValueError("Checkpoint directory {0} does not seem to exist".format(tdir))
     ck = os.path.join(tdir, "checkpoint-{0}".format(flags.load))
-    if not os.path.isfile(ck + ".npz"):
+    if not (os.path.isfile(ck + ".index") or os.path.isfile(ck + ".npz")):
         raise ValueError("Asked to load checkpoint {0}, but it does not seem to exist".format(flags.load))
     print("Loading model {0}".format(ck))
     model.saver.restore(session, ck)

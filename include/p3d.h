@@ -277,6 +277,11 @@ int64_t p3d_moments_workspace(int64_t F, int32_t D);
 int p3d_moments(const double* x, int64_t F, int32_t D, double* mean, double* stdv, void* work,
                 int64_t work_bytes, void* stream);
 
+/* CRC-32C (Castagnoli) of host memory -- TF tensor-bundle checksums (checkpoint interop,
+ * src/predict_3dpose.py:165-181,328 save/restore through tf.train.Saver).  crc = 0 starts a
+ * buffer; pass a previous result to continue it.  Host only, no device work. */
+uint32_t p3d_crc32c(const void* data, int64_t n, uint32_t crc);
+
 #ifdef __cplusplus
 }
 #endif

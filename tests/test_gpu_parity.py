@@ -354,6 +354,45 @@ def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, monkeyp
     plain.close()
 
 
+def test_tf_checkpoint_save_restore(tmp_path):
+    """Saver.save writes a TensorFlow V2 checkpoint (checkpoint-N.index / .data-00000-of-00001
+    + the `checkpoint` state file, tf_bundle.py) holding every tf.global_variables() name with
+    TF dtypes (global_step int32); restore into a fresh model gives the same state, and the
+    next training step of both models is bit-identical.  create_model(--load N) finds it the
+    way the reference does (src/predict_3dpose.py:165-181)."""
+    import checkpoint_io
+    import tf_bundle
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    rng = np.random.default_rng(2)
+    for _ in range(3):
+        m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 0.5, isTraining=True)
+    path = m.saver.save(None, str(tmp_path / "checkpoint"), global_step=3)
+    assert os.path.isfile(path + ".index") and os.path.isfile(path + ".data-00000-of-00001")
+    assert tf_bundle.read_checkpoint_state(str(tmp_path)) == path
+    raw = tf_bundle.read_bundle(path)
+    assert set(raw) == set(checkpoint_io.global_order(m.param_table))
+    assert raw["global_step"].dtype == np.int32 and int(raw["global_step"]) == 3
+    assert raw["linear_model/w1"].dtype == np.float32 and raw["linear_model/w1"].shape == (32, 256)
+    full = m.get_state()
+    _, m2 = make(cfg, model_seed=m.seed)
+    m2.saver.restore(None, path)
+    s2 = m2.get_state()
+    for k in full:
+        np.testing.assert_array_equal(np.asarray(full[k]), np.asarray(s2[k]), err_msg=k)
+    x, t = rng.standard_normal((64, 32)), rng.standard_normal((64, 48))
+    o1 = m.step(None, x, t, 0.5, isTraining=True)[3]
+    o2 = m2.step(None, x, t, 0.5, isTraining=True)[3]
+    np.testing.assert_array_equal(o1, o2)
+    bad = dict(raw)
+    bad["linear_model/w1"] = np.zeros((16, 256), np.float32)
+    tf_bundle.write_bundle(str(tmp_path / "bad"), bad)
+    with pytest.raises(ValueError):
+        m2.saver.restore(None, str(tmp_path / "bad"))
+    for mm in (m, m2):
+        mm.close()
+
+
 def test_npy_dump_round_trip(tmp_path):
     """Reference npy-dump export / import (trainable and global variables)."""
     import checkpoint_io

@@ -37,9 +37,9 @@ def main():
     lib.p3d_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = np.zeros(4096 * 8, np.uint64)
     assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
-    t = buf[:64 * 128].astype(np.int64).reshape(32, 2, 128)
+    t = buf[:64 * 2 * 128].astype(np.int64).reshape(64, 2, 128)
     NH = 4
-    live = [(g, r) for g in range(32) for r in range(2) if t[g, r, 0] and t[g, r, 8 * (NH + 1)]]
+    live = [(g, r) for g in range(64) for r in range(2) if t[g, r, 0] and t[g, r, 8 * (NH + 1)]]
     t0 = min(t[g, r, 0] for g, r in live)
     us = lambda v: round((v - t0) / 100.0, 2)   # noqa: E731
     out = []
@@ -56,7 +56,7 @@ def main():
         cyc = sum(row[64 + 8 * p + 1] - row[64 + 8 * p] for p in range(1, NH + 1))
         wall = sum(row[8 * p + 1] - row[8 * p] for p in range(1, NH + 1))
         out.append({"group": g, "row": r, "clock_ghz": round(cyc / max(wall, 1) / 10.0, 3), "start": us(row[0]), "census": us(row[1]), "input": us(row[2]),
-                    "handoff0": us(row[3]), "end_phase": [us(row[8 * p + 4]) for p in range(1, NH + 1)],
+                    "consts": us(row[4]), "in_mfma": us(row[5]), "handoff0": us(row[3]), "end_phase": [us(row[8 * p + 4]) for p in range(1, NH + 1)],
                     "reduce_end": us(row[8 * (NH + 1)]), "phases_us": ph})
     out.sort(key=lambda d: d["reduce_end"])
     for d in out:
