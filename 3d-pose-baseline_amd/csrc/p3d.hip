@@ -2195,27 +2195,32 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
 // smallest group; its epilogue constants of at most ECT tiles sit in LDS, p3d_serve6.h).
 struct Serve6Plan { int S = 0, rt = 4, ncm = 0; };
 
+// the built (RT, NCM) forms: batch-64 units with 2 / 4 / 7 / 8 column tiles per CU, half-step
+// units with 11, and XCD-wide units (S = 1, 2 tiles per CU) of 6 .. 16 row tiles
 static int serve6_ncm_for(int rt, int need) {
   if (rt == 2) return need <= 11 ? 11 : 0;
-  return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : need <= 8 ? 8 : 0;
+  if (rt == 4) return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : need <= 8 ? 8 : 0;
+  return need <= 2 ? 2 : 0;
 }
 
 // The plan minimising (rounds of units) x (fixed cost per phase + cost per column tile x tiles
 // per CU), 32 CUs per XCD (grid / 8): a phase's fixed cost (hand-off, ring fill, K-combine,
-// epilogue) ~4 us, a column tile of K = 1024 ~3.9 us at 4 row tiles (round-1 phase traces,
-// DESIGN.md 5a) and ~0.55 of that at 2 (the weight fragments serve half the rows).  B rows:
-// 20 batch-64 steps (1280 rows) -> RT = 2, S = 5: 40 units on 40 groups of 6-7 CUs, <= 11 tiles
-// each; 8 steps -> RT = 4, S = 1; 16 -> RT = 4, S = 2.
+// epilogue) ~4 us, a column tile of K = 1024 ~3.9 us at 4 row tiles, proportional to the row
+// tiles (round-1 phase traces).  20 batch-64 steps (1280 rows): RT = 10, S = 1 --
+// 160 rows per XCD, 2 column tiles per CU (the half-step form, RT = 2 with 5 groups per XCD,
+// costs 11 tiles of 2 row tiles per CU: 22 vs 20 tile-units and 5x the weight reads).
 static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
+  static const int rts[] = {4, 2, 6, 8, 10, 12, 16};
   const int cx = std::max(1, m->serve_grid / 8);
   const double cfix = 4.0;
   Serve6Plan best;
   double bt = 1e30;
-  for (int rt = 4; rt >= 2; rt -= 2) {
+  for (int rt : rts) {
     if (m->serve6_rt && m->serve6_rt != rt) continue;
+    if (rt > 4 && (T / 4) % 4 != 0) continue;   // the XCD-wide forms run a 4-deep weight ring
     const int64_t nb = (B + 16 * rt - 1) / (16 * rt);
-    const double ctile = (rt == 4 ? 3.9 : 0.55 * 3.9) * T / 64.0;
-    for (int S = 1; S <= (rt == 4 ? 4 : 8); ++S) {
+    const double ctile = 3.9 * (rt / 4.0) * T / 64.0;
+    for (int S = 1; S <= 8; ++S) {
       if (m->serve6_split && m->serve6_split != S) continue;
       const int nmin = cx / S;
       if (nmin < 1) continue;
@@ -2231,9 +2236,14 @@ static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
 
 static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, int rt, unsigned grid,
                           hipStream_t st, const ServeArgs& a) {
-  if (rt == 2) {   // 32-row units, 11 column tiles (S = 5)
-    go(ps, k_serve6<2, 3, 11, 2>, dim3(grid), dim3(256), st, a);
-    return;
+  switch (rt) {   // half-step units (11 column tiles, S = 5) / XCD-wide units (2 tiles, S = 1)
+    case 2: go(ps, k_serve6<2, 3, 11, 2>, dim3(grid), dim3(256), st, a); return;
+    case 6: go(ps, k_serve6<4, 3, 2, 6>, dim3(grid), dim3(256), st, a); return;
+    case 8: go(ps, k_serve6<4, 3, 2, 8>, dim3(grid), dim3(256), st, a); return;
+    case 10: go(ps, k_serve6<4, 3, 2, 10>, dim3(grid), dim3(256), st, a); return;
+    case 12: go(ps, k_serve6<4, 3, 2, 12>, dim3(grid), dim3(256), st, a); return;
+    case 16: go(ps, k_serve6<4, 3, 2, 16>, dim3(grid), dim3(256), st, a); return;
+    default: break;
   }
   // ring depth 4 for the narrow forms; 2 for 7 / 8 tiles (depth 4 spills there: 77 / 136
   // registers; depth 2 none / 38)
@@ -2329,9 +2339,11 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   if (use6) {
     const int T = L / 16;
     const int ncm = plan.ncm;
-    const int depth = plan.rt == 2 ? 2 : ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
-    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) +
-                     (plan.rt == 2 ? ", 2>" : ", 4>");
+    int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
+    if (plan.rt == 2) depth = 2;
+    if (plan.rt > 4) depth = 4;
+    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ", " +
+                     std::to_string(plan.rt) + ">";
     ProfScope ps(m, "serve");
     launch_serve6(ps, m, ncm, depth, plan.rt, (unsigned)m->serve_grid, st, a);
   } else {

@@ -73,18 +73,24 @@ __global__ __launch_bounds__(256) void k_serve_prep(ServeArgs p, float* ecg) {
 // owner of column tile t when T tiles are dealt contiguously over n members
 __device__ __forceinline__ int p3d_tile_owner(int t, int n, int T) { return ((t + 1) * n - 1) / T; }
 
-// RT: row tiles per step unit (4: the batch-64 step; 2: half a step, 32 rows -- rows are
-// independent in evaluation, so a launch of nb batch-64 steps may run as 2 nb units of 32 rows:
-// 20 steps = 40 units = 5 groups on each of the 8 XCDs, no group idle; p3d.hip serve6_plan)
+// RT: row tiles per unit.  Rows are independent in evaluation, so the rows of a launch need
+// not go in batch-64 steps: a unit of 16 RT rows is what one group runs through all layers.
+// RT = 4 is the batch-64 step; RT = 2 half a step (20 steps = 40 units = 5 groups per XCD);
+// RT = 6 .. 16 with S = 1 gives each XCD ONE unit of all its rows and all 32 of its CUs, each
+// CU 2 of a layer's 64 column tiles for every row tile (20 steps: 160 rows per XCD, RT = 10):
+// no group idles, no CU holds more tiles than another, and each weight fragment is read by one
+// CU per XCD and serves 10 row tiles (p3d.hip serve6_plan picks the form per launch).
+// The epilogue / input-layer work of a chunk, RT x NCM 16 x 16 tiles, is dealt to the waves
+// round-robin: unit u = w + 4 j is row tile u / NCM of column tile u % NCM (UMAX per wave).
 template <int DEPTH, int NDT, int NCM, int RT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve6(ServeArgs p) {
-  static_assert(RT == 4 || RT == 2, "row tiles per unit");
+  static_assert(RT >= 1 && RT <= 16, "row tiles per unit");
   constexpr int RE = P3D_SERVE6_RE;
   constexpr int ROWS = 16 * RT;              // rows of one unit
-  constexpr int WPR = 4 / RT;                // waves per row tile in the epilogue / input layer
+  constexpr int UMAX = (RT * NCM + 3) / 4;   // 16 x 16 tiles a wave finishes per chunk
   constexpr int PT = RT * NDT * 256;         // floats of one tile's output partial
   constexpr int E4 = RT * NDT * 64;          // float4 elements of a unit's output
-  constexpr int DA = NCM >= 7 && DEPTH > 2 ? 2 : DEPTH;   // activation ring depth
+  constexpr int DA = (NCM >= 7 || RT >= 6) && DEPTH > 2 ? 2 : DEPTH;   // activation ring depth
 #ifndef P3D_S6_PD
   constexpr int PD = NCM <= 4 ? 2 : 1;       // ring slots prefetched off-contraction
 #else
@@ -107,8 +113,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
   const int q4 = 4 * (lane >> 4);
   const int S = p.split;
-  // the row tile this wave finishes, and which of the chunk's tiles (cc % WPR == csel)
-  const int rtw = w % RT, csel = w / RT;
 #ifdef P3D_TRACE
   const unsigned long long t_start = wall_clock64();
   unsigned long long* tr6 = nullptr;
@@ -171,24 +175,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool split_red = t_lo < t_hi && ecnt <= 64 * RE;
 
   bool trs = true;                           // stamping this step (the group's first)
-  auto in_issue = [&](int64_t rbase, int c0, f32x4 (&xa)[4], f32x4 (&wb)[NCM][4]) {
-    int64_t rowc = rbase + 16 * rtw + (lane & 15);
-    rowc = rowc < p.M ? rowc : p.M - 1;
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      if (g < ngK0) xa[g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+  // input layer of the chunk at c0 for the unit at rbase: this wave's tiles (unit j: row tile
+  // (w + 4 j) / NCM, column tile c0 + (w + 4 j) % NCM), both operands of each per k-group
+  auto in_issue = [&](int64_t rbase, int c0, f32x4 (&xa)[UMAX][4], f32x4 (&wb)[UMAX][4]) {
     const int nck = min(NCM, t_hi - c0);
 #pragma unroll
-    for (int cc = 0; cc < NCM; ++cc) {
+    for (int j = 0; j < UMAX; ++j) {
+      const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+      int64_t rowc = rbase + 16 * rt + (lane & 15);
+      rowc = rowc < p.M ? rowc : p.M - 1;
       const int t = c0 + (cc < nck ? cc : nck - 1);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        if (g < ngK0) wb[cc][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
+        if (g < ngK0) {
+          xa[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+          wb[j][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
+        }
     }
   };
   // the group's first step's input-layer operands, requested before the epilogue constants
   // are copied (their latencies overlap)
-  f32x4 xa0[4], wb0[NCM][4];
+  f32x4 xa0[UMAX][4], wb0[UMAX][4];
   if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * ROWS, t_lo, xa0, wb0);
   {   // epilogue constants of this member's tiles, formed once per launch: bias, inv = gamma /
       // sqrt(var + eps), shift = beta - mean * inv (the arithmetic of every other path), and
@@ -277,26 +284,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // input layer (K0 = input_size <= 64) of the member's tiles for the rows of the step at
   // rbase, row tile w, into act buffer cbuf: the rows loaded once, then every tile's weight
   // fragments requested before the first MFMA (one round of load latency, not one per tile)
-  auto in_compute = [&](int c0, const f32x4 (&xa)[4], const f32x4 (&wb)[NCM][4], int cbuf) {
+  auto in_compute = [&](int c0, const f32x4 (&xa)[UMAX][4], const f32x4 (&wb)[UMAX][4], int cbuf) {
     const int nck = min(NCM, t_hi - c0);
 #pragma unroll
-    for (int cc = 0; cc < NCM; ++cc) {
-      if (cc >= nck || cc % WPR != csel) continue;
+    for (int j = 0; j < UMAX; ++j) {
+      const int u = w + 4 * j, rt = u / NCM, cc = u % NCM;
+      if (u >= RT * NCM || cc >= nck) continue;
       const int t = c0 + cc;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         if (g < ngK0)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[cc][g][e], xa[g][e], acc, 0, 0, 0);
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[j][g][e], xa[j][g][e], acc, 0, 0, 0);
       if (wsq_any) maxnorm_div(0, acc);
       const f32x4 y = epi_t(0, t - t_lo, acc);
-      *(f32x4*)(act + cbuf * slab + ((int64_t)(rtw * ngL + t) * 64 + lane) * 4) = y;
+      *(f32x4*)(act + cbuf * slab + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = y;
     }
   };
   auto in_layer = [&](int64_t rbase, int cbuf, int cfrom) {
     for (int c0 = cfrom; c0 < t_hi; c0 += NCM) {
-      f32x4 xa[4], wb[NCM][4];
+      f32x4 xa[UMAX][4], wb[UMAX][4];
       in_issue(rbase, c0, xa, wb);
       in_compute(c0, xa, wb, cbuf);
     }
@@ -478,13 +486,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // requested unconditionally (the residual operands from A where there is no residual,
         // W4 in every phase): conditional loads would make the compiler's vmcnt waits
         // conservative, i.e. wait for the next ring's weights behind them as well
-        f32x4 rv[NCM], wo[NCM][NDT];
+        f32x4 rv[UMAX], wo[UMAX][NDT];
         const __amdgpu_buffer_rsrc_t rr = p3d_rsrc(res ? res : A);
 #pragma unroll
-        for (int cc = 0; cc < NCM; ++cc) {
+        for (int j = 0; j < UMAX; ++j) {
+          const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
           const int t = c0 + (cc < nck ? cc : nck - 1);
-          rv[cc] = p3d_ld_sc1(rr, (int)(((int64_t)(rtw * ngL + t) * 64 + lane) * 16));
-          p3d_wo_load<NDT>(lo, t, ngL, wo[cc]);
+          rv[j] = p3d_ld_sc1(rr, (int)(((int64_t)(rt * ngL + t) * 64 + lane) * 16));
+          p3d_wo_load<NDT>(lo, t, ngL, wo[j]);
         }
         // the next contraction's first weight slots: this member's next chunk, the next
         // layer, or the next step's first layer (requested even after a group's last step:
@@ -501,33 +510,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int t = 0; t < RT; ++t) red[((w * RT + t) * NCM + cc) * 64 + lane] = acc[cc][t];
         __syncthreads();
         P3D_S6_STAMP(trs && first_c, 8 * ph + 2);
-        f32x4 sacc[NCM];                       // K slices summed in slice order
+        f32x4 sacc[UMAX];                      // K slices summed in slice order, this wave's tiles
 #pragma unroll
-        for (int cc = 0; cc < NCM; ++cc) {
-          if (cc % WPR != csel) { sacc[cc] = f32x4{0.f, 0.f, 0.f, 0.f}; continue; }
-          sacc[cc] = red[((0 * RT + rtw) * NCM + cc) * 64 + lane];   // slice 0, tile (rtw, cc)
+        for (int j = 0; j < UMAX; ++j) {
+          const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+          sacc[j] = red[((0 * RT + rt) * NCM + cc) * 64 + lane];   // slice 0, tile (rt, cc)
 #pragma unroll
-          for (int k = 1; k < 4; ++k) sacc[cc] += red[((k * RT + rtw) * NCM + cc) * 64 + lane];
+          for (int k = 1; k < 4; ++k) sacc[j] += red[((k * RT + rt) * NCM + cc) * 64 + lane];
         }
         if (wsq_any)
 #pragma unroll
-          for (int cc = 0; cc < NCM; ++cc) maxnorm_div(ph, sacc[cc]);
+          for (int j = 0; j < UMAX; ++j) maxnorm_div(ph, sacc[j]);
 #pragma unroll
-        for (int cc = 0; cc < NCM; ++cc) {
-          if (cc >= nck || cc % WPR != csel) continue;
+        for (int j = 0; j < UMAX; ++j) {
+          const int u = w + 4 * j, rt = u / NCM, cc = u % NCM;
+          if (u >= RT * NCM || cc >= nck) continue;
           const int t = c0 + cc;
-          f32x4 yv = epi_t(ph, t - t_lo, sacc[cc]);
-          if (res) yv += rv[cc];
+          f32x4 yv = epi_t(ph, t - t_lo, sacc[j]);
+          if (res) yv += rv[j];
           if (lastp) {                         // fused output layer: this tile's 64 x 48 partial
 #pragma unroll
             for (int o = 0; o < NDT; ++o) {
               f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[cc][o][e], pacc, 0, 0, 0);
-              *(f32x4*)(pdst + (int64_t)t * PT + ((rtw * NDT + o) * 64 + lane) * 4) = pacc;
+              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[j][o][e], pacc, 0, 0, 0);
+              *(f32x4*)(pdst + (int64_t)t * PT + ((rt * NDT + o) * 64 + lane) * 4) = pacc;
             }
           } else {
-            *(f32x4*)(Y + ((int64_t)(rtw * ngL + t) * 64 + lane) * 4) = yv;
+            *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
           }
         }
         // red / rsum are rewritten by this member's next contraction of the phase

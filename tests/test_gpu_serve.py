@@ -158,16 +158,17 @@ def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1, rt=None):
 def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
     """k_serve6 (launches of <= 32 steps; the driver's 20-step headline): 1-4 groups per XCD of
     batch-64 units (16-column tiles dealt contiguously, 7 tiles per CU at 3 groups) and 32-row
-    half-step units at 5 (and 3) groups per XCD give the same bits -- the association of every
-    sum is fixed by the tile, not by the group or unit shape -- and the oracle's outputs; the
-    auto choice for 20 steps is 40 half-step units on 5 groups per XCD (no group idle)."""
+    half-step units at 5 (and 3) groups per XCD, and XCD-wide units of 6 / 8 / 16 row tiles give
+    the same bits -- the association of every sum is fixed by the tile, not by the group or unit
+    shape -- and the oracle's outputs; the auto choice for 20 steps is one unit of 160 rows per
+    XCD on all 32 of its CUs, 2 column tiles each."""
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     B = 64 * 20
     x = np.random.default_rng(620).standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
     outs = {}
-    for split, rt in ((None, None), (1, 4), (2, 4), (3, 4), (4, 4), (5, 2), (3, 2)):
+    for split, rt in ((None, None), (1, 4), (2, 4), (3, 4), (4, 4), (5, 2), (3, 2), (1, 6), (1, 8), (1, 16)):
         st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
         y = m.serve_device(xd)
         torch.cuda.synchronize()
@@ -178,7 +179,7 @@ def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
         outs[(split, rt)] = (y, name.value.decode())
         m.close()
     auto = outs[(None, None)]
-    assert auto[1] == "k_serve6<2, 3, 11, 2>", auto[1]     # 20 steps -> 40 half steps, 5 groups per XCD
+    assert auto[1] == "k_serve6<4, 3, 2, 10>", auto[1]     # 20 steps -> one 160-row unit per XCD
     assert outs[(3, 4)][1] == "k_serve6<2, 3, 7, 4>", outs[(3, 4)][1]
     for key, (y, _) in outs.items():
         assert torch.equal(y, auto[0]), key
@@ -210,7 +211,7 @@ def test_serve6_launch_sizes_vs_oracle(B):
     (1024, 2, True, True, False, True),      # --predict_14
     (2048, 1, True, True, False, False),     # 128 tiles: 13 per CU at 3 groups -> two contractions
 ])
-@pytest.mark.parametrize("split,rt", [(None, None), (3, 4), (5, 2)])
+@pytest.mark.parametrize("split,rt", [(None, None), (3, 4), (5, 2), (1, 10)])
 def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split, rt):
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
                       predict_14=p14)
@@ -224,7 +225,7 @@ def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_
     m.close()
 
 
-@pytest.mark.parametrize("split,rt", [(1, 4), (2, 4), (3, 4), (5, 2)])
+@pytest.mark.parametrize("split,rt", [(1, 4), (2, 4), (3, 4), (5, 2), (1, 10)])
 def test_serve6_many_steps_per_group(monkeypatch, split, rt):
     """k_serve6 forced on a long launch (P3D_SERVE6=2): every group runs many steps, so the
     next step's input layer rides in the last phase and each step's output is reduced in the
