@@ -1303,6 +1303,8 @@ struct p3d_model {
   float* serve_buf = nullptr;
   unsigned serve_epoch = 0;     // k_serve6 launches so far (sync-word bank = epoch & 1)
   bool serve_banks_clean = true;   // both banks zero (false after a k_serve5 launch used bank 0)
+  float* serve_ecg = nullptr;      // k_serve6 epilogue-constant table (k_serve_prep), [layer][tile][48] + divisors
+  bool serve_ec_dirty = true;      // parameters or moving statistics changed since the table was formed
   unsigned* serve_sync = nullptr;
   int* serve_err = nullptr;
   int serve_grid = 0;
@@ -1367,6 +1369,7 @@ void free_all(p3d_model* m) {
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
+  if (m->serve_ecg) (void)hipFree(m->serve_ecg);
   if (m->xsync) (void)hipFree(m->xsync);
 }
 // ---- teardown in any order -------------------------------------------------------------
@@ -1705,6 +1708,7 @@ extern "C" int p3d_flat_ptr(p3d_model* m, int32_t which, void** dptr, int64_t* n
 }
 
 static int refresh_derived(p3d_model* m, hipStream_t st) {
+  m->serve_ec_dirty = true;
   if (m->cfg.dtype == P3D_DTYPE_BF16) {
     for (const Layer& ly : m->layers) {
       const int NP = (ly.N + 15) / 16 * 16;
@@ -2106,6 +2110,7 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
     in = a.Y;
   }
   if (training) {
+    m->serve_ec_dirty = true;   // moving statistics updated (UPDATE_OPS)
     m->have_cache = true;
     m->x_cached = x;
     m->B_cached = B;
@@ -2294,6 +2299,10 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if ((e = hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     m->serve_err = (int*)(m->serve_sync + 2 * P3D_SERVE_SYNC_WORDS);
+    const int64_t necg = (int64_t)(2 * c.num_layers + 2) * (L / 16) * 48 + 64;
+    if ((e = hipMalloc(&m->serve_ecg, necg * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    m->serve_ec_dirty = true;
   }
   ServeArgs a{};
   a.x = x; a.y = y; a.M = B; a.nb = (int)((B + 63) / 64);   // batch-64 steps (k_serve6 may halve them)
@@ -2319,6 +2328,17 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     a.split = plan.S;
     use6 = plan.S > 0;                       // no form covers this width: k_serve5
     if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
+  }
+  a.ecg = m->serve_ecg;
+  if (use6 && m->serve_ec_dirty) {
+    // the epilogue-constant table, formed once per parameter version (refresh_derived, a
+    // training forward and every Adam step mark it stale): steady-state calls are one launch
+    const int nl = 2 * c.num_layers + 1, nthreads = std::max(nl * L, (int)P3D_SERVE_SYNC_WORDS);
+    ServeArgs pa = a;
+    pa.sync = m->serve_sync + (m->serve_epoch & 1u) * P3D_SERVE_SYNC_WORDS;   // the bank this launch uses: zero
+    k_serve_prep<<<(unsigned)((nthreads + 255) / 256), 256, 0, st>>>(pa, m->serve_ecg);
+    LAUNCH_CHECK("k_serve_prep");
+    m->serve_ec_dirty = false;
   }
   if (use6) {
     // no memset in front: this launch's bank was zeroed by the previous k_serve6 launch (or at
@@ -2689,6 +2709,7 @@ extern "C" int p3d_train_step(p3d_model* m, const float* x, const float* t, int6
 }
 
 static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st) {
+  m->serve_ec_dirty = true;
   AdamArgs a{};
   a.w = m->flat[0]; a.g = m->flat[1]; a.m = m->flat[2]; a.v = m->flat[3];
   a.wpk = m->wpk; a.st = m->dstate;

@@ -111,6 +111,7 @@ struct ServeArgs {
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)
   unsigned* sync_next; // k_serve6: the other sync-word bank, zeroed by this launch for the next
+  const float* ecg;    // k_serve6: epilogue constants per layer and 16-column tile (k_serve_prep)
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 

@@ -197,43 +197,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // are copied (their latencies overlap)
   f32x4 xa0[UMAX][4], wb0[UMAX][4];
   if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * ROWS, t_lo, xa0, wb0);
-  {   // epilogue constants of this member's tiles, formed once per launch: bias, inv = gamma /
-      // sqrt(var + eps), shift = beta - mean * inv (the arithmetic of every other path), and
-      // each layer's max-norm divisor.  Every thread's operand loads are issued before the
-      // first is used (one round of load latency, overlapping the input layer's).
-    const int nl = NH + 1, tot = nl * ECT * 16;
-    constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 16 + 255) / 256;
-    float vb[ECN], vg[ECN], vbe[ECN], vm[ECN], vv[ECN];
+  {   // epilogue constants of this member's tiles -- bias, inv = gamma / sqrt(var + eps),
+      // shift = beta - mean * inv (the arithmetic of every other path), each layer's max-norm
+      // divisor -- copied from the table k_serve_prep forms once per parameter version (one
+      // round of loads, no per-launch arithmetic)
+    const int nl = NH + 1, tot = nl * ECT * 48;
+    constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
+    float v[ECN];
 #pragma unroll
     for (int k = 0; k < ECN; ++k) {
       const int idx = tid + 256 * k;
-      const int l = idx / (ECT * 16), rem = idx % (ECT * 16), cs = rem >> 4, j = rem & 15;
-      const int col = 16 * min(t_lo + cs, T - 1) + j;
-      vb[k] = vg[k] = vbe[k] = vm[k] = 0.f;
-      vv[k] = 1.f;
-      if (idx < tot) {
-        const ServeLayer& lyc = p.ly[l];
-        vb[k] = lyc.bias[col];
-        if (p.bn) { vg[k] = lyc.gamma[col]; vbe[k] = lyc.beta[col]; vm[k] = lyc.mmean[col]; vv[k] = lyc.mvar[col]; }
-      }
+      const int l = idx / (ECT * 48), rem = idx % (ECT * 48), cs = rem / 48, j = rem % 48;
+      v[k] = idx < tot ? p.ecg[((int64_t)l * T + min(t_lo + cs, T - 1)) * 48 + j] : 0.f;
     }
-    float wq = 1.f;
-    if (tid < nl && wsq_any) wq = *p.ly[tid].wsq;
+    const float wq = tid < nl ? p.ecg[(int64_t)nl * T * 48 + tid] : 1.f;
 #pragma unroll
-    for (int k = 0; k < ECN; ++k) {
-      const int idx = tid + 256 * k;
-      if (idx < tot) {
-        const int l = idx / (ECT * 16), rem = idx % (ECT * 16), cs = rem >> 4, j = rem & 15;
-        float inv = 1.f, shift = 0.f;
-        if (p.bn) {
-          inv = (1.0f / sqrtf(vv[k] + p.eps)) * vg[k];
-          shift = vbe[k] - vm[k] * inv;
-        }
-        float* e = ec + (l * ECT + cs) * 48;
-        e[j] = vb[k]; e[16 + j] = inv; e[32 + j] = shift;
-      }
-    }
-    if (tid < nl) ecm[tid] = wsq_any ? fmaxf(sqrtf(wq), 1.0f) : 1.0f;
+    for (int k = 0; k < ECN; ++k)
+      if (tid + 256 * k < tot) ec[tid + 256 * k] = v[k];
+    if (tid < nl) ecm[tid] = wq;
     __syncthreads();
   }
   P3D_S6_STAMP(trs, 4);

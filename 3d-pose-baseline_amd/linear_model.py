@@ -396,6 +396,8 @@ class LinearModel(object):
         evaluation and checkpoint; a no-op on one GPU."""
         if self.data_parallel:
             dist_utils.allreduce_mean_(self.flat["moving"])
+            # derived device state (the serve path's BN constants) follows the new statistics
+            check(lib().p3d_params_updated(self._h, self.stream()), "p3d_params_updated")
 
     def broadcast_parameters(self):
         """Rank 0's variables to every rank (start of data-parallel training)."""

@@ -250,3 +250,27 @@ def test_serve6_many_steps_per_group(monkeypatch, split, rt):
     assert torch.equal(m6.serve_device(xd[:64 * 20]), y6[:64 * 20])
     m6.close()
     m5.close()
+
+
+def test_serve6_constants_follow_parameter_updates():
+    """k_serve6 reads its epilogue constants (bias, BN inv / shift, max-norm divisors) from a
+    table formed once per parameter version: after a training step (new weights, new moving
+    statistics) and after set_weights, the next serve launch agrees with the eval forward of
+    the updated model, not with the stale table."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True, max_norm=True)
+    st, m = make(cfg, max_batch=64 * 20)
+    rng = np.random.default_rng(31)
+    xd = torch.from_numpy(rng.standard_normal((64 * 20, 32)).astype(np.float32)).cuda()
+    y0 = m.serve_device(xd).clone()
+    m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 0.5, isTraining=True)
+    y1 = m.serve_device(xd).clone()
+    m.serve_check()
+    assert not torch.equal(y0, y1)
+    close(y1.cpu().numpy(), m.forward_device(xd, False, 1.0).cpu().numpy(), atol=5e-5, rtol=5e-5)
+    st2 = ref_mlp.init_state(cfg, seed=9, bn_seed=10)
+    m.set_weights({**st2.params, **st2.moving})
+    y2 = m.serve_device(xd)
+    m.serve_check()
+    ro, _ = ref_mlp.forward(st2, xd.cpu().numpy(), False, 1.0, 0, 0, 0)
+    close(y2.cpu().numpy(), ro)
+    m.close()

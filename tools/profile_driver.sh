@@ -1,0 +1,15 @@
+#!/bin/bash
+# Profiles of the driver's headline command (run on the GPU box from the repo root):
+#   1. rocprofv3 --kernel-trace --stats of `python3 bench.py --gpus 1 --steps 20 --warmup 5`
+#   2. two separate PMC passes (FETCH_SIZE, WRITE_SIZE) of the serve path alone at 20 steps
+#      per launch (tools/pmc_traffic.py turns them into HBM bytes per launch)
+# Every step under its own time limit; the script stops at the first failure.
+set -e
+OUT=${1:-gpurun_out/prof}
+mkdir -p "$OUT"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_under_rocprof.json" 2> "$OUT/bench_under_rocprof.err"
+SERVE="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-streams --no-eval --no-data --no-api --no-stress --train-steps 0 --no-cpu"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- $SERVE > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- $SERVE > "$OUT/write.json" 2> "$OUT/write.err"
+echo profile-done
