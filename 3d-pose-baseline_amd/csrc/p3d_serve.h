@@ -128,13 +128,20 @@ __device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_o
 // rank within its XCD (one returning atomic on that XCD's counter), then a wait until the
 // eight counters sum to the grid (every workgroup resident, every count final).  sh[0] = XCD,
 // sh[1] = rank, sh[8 + x] = workgroups on XCD x, sh[2] = 1 if the wait timed out or an XCD
-// holds more than maxn workgroups (the flag barriers poll one lane per member).
-__device__ __forceinline__ void p3d_serve_census(const ServeArgs& p, int* sh, int maxn) {
+// holds more than maxn workgroups (the flag barriers poll one lane per member).  In two
+// halves, so a kernel can do independent work between its arrival and the wait.
+__device__ __forceinline__ void p3d_serve_census_arrive(const ServeArgs& p, int* sh) {
   if (threadIdx.x == 0) {
     unsigned xr;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
     const int xcc = (int)(xr & 7u);
-    const unsigned rank = __hip_atomic_fetch_add(p.sync + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = xcc;
+    sh[1] = (int)__hip_atomic_fetch_add(p.sync + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void p3d_serve_census_wait(const ServeArgs& p, int* sh, int maxn) {
+  if (threadIdx.x == 0) {
     int bad = 0, spin = 0;
     unsigned c[8];
     while (true) {
@@ -148,14 +155,17 @@ __device__ __forceinline__ void p3d_serve_census(const ServeArgs& p, int* sh, in
       __builtin_amdgcn_s_sleep(1);
       if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
     }
-    sh[0] = xcc; sh[1] = (int)rank;
 #pragma unroll
     for (int x = 0; x < 8; ++x) sh[8 + x] = (int)c[x];
-    if ((int)c[xcc] > maxn) bad = 1;
+    if ((int)c[sh[0]] > maxn) bad = 1;
     if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh[2] = bad;
   }
   __syncthreads();
+}
+__device__ __forceinline__ void p3d_serve_census(const ServeArgs& p, int* sh, int maxn) {
+  p3d_serve_census_arrive(p, sh);
+  p3d_serve_census_wait(p, sh, maxn);
 }
 
 // ---- register ring -------------------------------------------------------------------

@@ -90,7 +90,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int UMAX = (RT * NCM + 3) / 4;   // 16 x 16 tiles a wave finishes per chunk
   constexpr int PT = RT * NDT * 256;         // floats of one tile's output partial
   constexpr int E4 = RT * NDT * 64;          // float4 elements of a unit's output
-  constexpr int DA = (NCM >= 7 || RT >= 6) && DEPTH > 2 ? 2 : DEPTH;   // activation ring depth
+  // activation ring depth (the wide forms cannot hold both rings DEPTH deep: 4 x 11 fragments
+  // spilled 77 registers at NCM = 7, RT = 4)
+  constexpr int DA = RT >= 6 ? (DEPTH >= 8 ? 4 : 2) : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);
 #ifndef P3D_S6_PD
   constexpr int PD = NCM <= 4 ? 2 : 1;       // ring slots prefetched off-contraction
 #else
@@ -126,27 +128,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     unsigned* other = p.sync_next;
     for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
   }
-  p3d_serve_census(p, sh, (S < 1 || S > 8) ? -1 : 64 * S);
-  if (!sh[2]) {
-  const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
-  const int nx = __builtin_amdgcn_readfirstlane(sh[8 + xcc]);
-  const int half = rx % S, r = rx / S;
-  const int n = (nx + S - 1 - half) / S;
-  const int gid = xcc * S + half;
-  // groups in order of decreasing size (h-major): with fewer steps than groups the larger
-  // groups -- fewer tiles per member -- take them
-  int ng = 0, gi = 0;
-  for (int h = 0; h < S; ++h)
+  // The census in two halves: after its arrival (XCD id, rank) a workgroup guesses its place
+  // assuming every XCD holds grid / 8 workgroups (the dispatcher's round-robin) and requests its
+  // first input-layer operands and epilogue constants; the wait for every workgroup's arrival
+  // then hides their latency.  The guess is used only if the final counts confirm it (every
+  // workgroup sees the same counts, so all decide alike); otherwise the loads are re-issued.
+  p3d_serve_census_arrive(p, sh);
+  const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
+  constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
+  // place of this workgroup for XCD counts cnt(x): member r of group gid (gi-th of ng groups
+  // taking units), its tiles [t_lo, t_hi)
+  auto place = [&](auto cnt, int xcc, int rx, int& r, int& n, int& gid, int& gi, int& ng) {
+    const int half = rx % S;
+    r = rx / S;
+    n = (cnt(xcc) + S - 1 - half) / S;
+    gid = xcc * S + half;
+    // groups in order of decreasing size (h-major): with fewer units than groups the larger
+    // groups -- fewer tiles per member -- take them
+    ng = 0;
+    gi = 0;
+    for (int h = 0; h < S; ++h)
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      const int cnt = (__builtin_amdgcn_readfirstlane(sh[8 + x]) + S - 1 - h) / S;
-      if (cnt > 0) { if (x == xcc && h == half) gi = ng; ++ng; }
+      for (int x = 0; x < 8; ++x) {
+        const int c = (cnt(x) + S - 1 - h) / S;
+        if (c > 0) { if (x == xcc && h == half) gi = ng; ++ng; }
+      }
+    if (p.max_groups > 0 && ng > p.max_groups) {
+      ng = p.max_groups;
+      if (gi >= ng) gi = p.nb;
     }
-  if (p.max_groups > 0 && ng > p.max_groups) {
-    ng = p.max_groups;
-    if (gi >= ng) gi = p.nb;
+    if ((T + n - 1) / n > ECT) gi = -1;      // a placement the host did not size this form for
+  };
+  // first-unit input-layer operands (this wave's tiles) and the epilogue-constant table rows
+  f32x4 xa0[UMAX][4], wb0[UMAX][4];
+  float vec[ECN], wq = 1.f;
+  auto prefetch = [&](int gi_, int tlo, int thi) {
+    if (gi_ >= 0 && gi_ < p.nb && tlo < thi) {
+      const int nck = min(NCM, thi - tlo);
+#pragma unroll
+      for (int j = 0; j < UMAX; ++j) {
+        const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+        int64_t rowc = (int64_t)gi_ * ROWS + 16 * rt + (lane & 15);
+        rowc = rowc < p.M ? rowc : p.M - 1;
+        const int t = tlo + (cc < nck ? cc : nck - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (g < ngK0) {
+            xa0[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
+            wb0[j][g] = *(const f32x4*)(p.ly[0].Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
+          }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < ECN; ++k) {
+      const int idx = tid + 256 * k;
+      const int l = idx / (ECT * 48), rem = idx % (ECT * 48), cs = rem / 48, j = rem % 48;
+      vec[k] = idx < tot_ec ? p.ecg[((int64_t)l * T + min(tlo + cs, T - 1)) * 48 + j] : 0.f;
+    }
+    wq = tid < nl_ec ? p.ecg[(int64_t)nl_ec * T * 48 + tid] : 1.f;
+  };
+  const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
+  const int nxg = (int)gridDim.x / 8;
+  const bool guessable = (gridDim.x % 8) == 0 && S >= 1 && S <= 8;
+  int g_r = 0, g_n = 1, g_gid = 0, g_gi = -1, g_ng = 0;
+  if (guessable) {
+    place([&](int) { return nxg; }, xcc, rx, g_r, g_n, g_gid, g_gi, g_ng);
+    prefetch(g_gi, (T * g_r) / g_n, (T * (g_r + 1)) / g_n);
   }
-  if ((T + n - 1) / n > ECT) {               // a placement the host did not size this form for:
+  p3d_serve_census_wait(p, sh, (S < 1 || S > 8) ? -1 : 64 * S);
+  if (!sh[2]) {
+  bool guess_held = guessable;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) guess_held = guess_held && __builtin_amdgcn_readfirstlane(sh[8 + x]) == nxg;
+  int r, n, gid, gi, ng;
+  place([&](int x) { return __builtin_amdgcn_readfirstlane(sh[8 + x]); }, xcc, rx, r, n, gid, gi, ng);
+  if (gi < 0) {                              // a placement the host did not size this form for:
     if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     gi = p.nb;                               // the whole group reports instead of computing
   }
@@ -193,28 +249,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
     }
   };
-  // the group's first step's input-layer operands, requested before the epilogue constants
-  // are copied (their latencies overlap)
-  f32x4 xa0[UMAX][4], wb0[UMAX][4];
-  if (gi < p.nb && t_lo < t_hi) in_issue((int64_t)gi * ROWS, t_lo, xa0, wb0);
+  // the guess failed: the first unit's operands and the constants again, for the real place
+  if (!guess_held) prefetch(gi, t_lo, t_hi);
   {   // epilogue constants of this member's tiles -- bias, inv = gamma / sqrt(var + eps),
       // shift = beta - mean * inv (the arithmetic of every other path), each layer's max-norm
-      // divisor -- copied from the table k_serve_prep forms once per parameter version (one
-      // round of loads, no per-launch arithmetic)
-    const int nl = NH + 1, tot = nl * ECT * 48;
-    constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
-    float v[ECN];
-#pragma unroll
-    for (int k = 0; k < ECN; ++k) {
-      const int idx = tid + 256 * k;
-      const int l = idx / (ECT * 48), rem = idx % (ECT * 48), cs = rem / 48, j = rem % 48;
-      v[k] = idx < tot ? p.ecg[((int64_t)l * T + min(t_lo + cs, T - 1)) * 48 + j] : 0.f;
-    }
-    const float wq = tid < nl ? p.ecg[(int64_t)nl * T * 48 + tid] : 1.f;
+      // divisor -- copied from the table k_serve_prep forms once per parameter version
 #pragma unroll
     for (int k = 0; k < ECN; ++k)
-      if (tid + 256 * k < tot) ec[tid + 256 * k] = v[k];
-    if (tid < nl) ecm[tid] = wq;
+      if (tid + 256 * k < tot_ec) ec[tid + 256 * k] = vec[k];
+    if (tid < nl_ec) ecm[tid] = wq;
     __syncthreads();
   }
   P3D_S6_STAMP(trs, 4);

@@ -451,6 +451,30 @@ class LinearModel(object):
         check(lib().p3d_serve(self._h, ptr(x), B, ptr(out), self.stream()), "p3d_serve")
         return out
 
+    def serve_launcher(self, x, out):
+        """A zero-argument callable that launches p3d_serve on the fixed device buffers x
+        [B, input_size] and out [B, output_size] on the current stream -- the serve_device
+        call with its argument checks and conversions done once, for serving loops over static
+        buffers.  The buffers must outlive the callable."""
+        import ctypes
+        torch = self.torch
+        if not (isinstance(x, torch.Tensor) and x.dtype is torch.float32 and x.dim() == 2 and x.is_cuda and
+                x.is_contiguous() and x.shape[1] == self.input_size):
+            raise ValueError("serve_launcher: x must be a contiguous float32 [B, %d] device tensor" % self.input_size)
+        B = x.shape[0]
+        if not (isinstance(out, torch.Tensor) and out.dtype is torch.float32 and out.is_contiguous() and
+                tuple(out.shape) == (B, self.output_size) and out.is_cuda):
+            raise ValueError("serve_launcher: out must be a contiguous float32 [%d, %d] device tensor"
+                             % (B, self.output_size))
+        fn, args = lib().p3d_serve, (self._h, ctypes.c_void_p(x.data_ptr()), B,
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self.stream()))
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                check(rc, "p3d_serve")
+        return launch
+
     def serve_check(self):
         """Raise if a p3d_serve launch could not synchronise its workgroups (device read)."""
         check(lib().p3d_serve_check(self._h), "p3d_serve")
