@@ -610,21 +610,26 @@ struct BwdArgs {
   const float* lossp; int nlossp; // fused MSE: workgroup 0 folds the forward's loss partials
   float* loss; float loss_scale;  //   (fixed order) into loss[0] = scale * sum
   XchgSite xs; int xchg;          // with bnpart: exchange form (p3d_xchg.h) -- dz, dgamma, dbeta here
+  float* alpha_out; AdamFuse af;  // fused Adam: tile (0, 0) stores the step's alpha for later launches
 };
 
 // RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
 // RS = 1: 16x16 tiles over a (K/16, M/16) grid, BN sums left as row-tile partials (bnpart).
+// The body on tile (bx, by) of a (K/16, gy) grid; k_dgrad runs it on its own grid, k_dgrad_wg
+// beside weight-gradient tiles of the layer above.
 template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
-__global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
+__device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by, int gy) {
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int ct = blockIdx.x, n0 = ct * 16, m0 = blockIdx.y * 16 * RS;
+  const int ct = bx, n0 = ct * 16, m0 = by * 16 * RS;
   const int col = n0 + i;
   const bool cok = col < p.K;
   const int cc = cok ? col : p.K - 1;
   const int ngK = p.K >> 4;
-  if (p.lossp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+  if (p.alpha_out && bx == 0 && by == 0 && threadIdx.x == 0)
+    *p.alpha_out = p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
+  if (p.lossp && bx == 0 && by == 0 && threadIdx.x == 0) {
     float l = 0.f;
     for (int k = 0; k < p.nlossp; ++k) l += p.lossp[k];
     p.loss[0] = l * p.loss_scale;
@@ -702,18 +707,18 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
     sg = p3d_colsum16(sg);
     sgx = p3d_colsum16(sgx);
     if (p.xchg) {   // exchange form: the row-tile siblings swap {sum g, sum g xhat}
-      const int R = (int)gridDim.y;
+      const int R = gy;
       float at[P3D_XCHG_MAXR], bt[P3D_XCHG_MAXR];
-      p3d_xchg_put(p.xs, p.K, blockIdx.y, col, q == 0 && cok, sg, sgx, xtag);
+      p3d_xchg_put(p.xs, p.K, by, col, q == 0 && cok, sg, sgx, xtag);
       p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt);
-      p3d_xchg_done(p.xs, blockIdx.y);
+      p3d_xchg_done(p.xs, by);
       sg = 0.f;
       sgx = 0.f;
 #pragma unroll
       for (int t = 0; t < P3D_XCHG_MAXR; ++t)
         if (t < R) { sg += at[t]; sgx += bt[t]; }
       if (!cok) return;
-      if (blockIdx.y == 0 && q == 0) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
+      if (by == 0 && q == 0) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
       const float fmx = (float)p.M;
 #pragma unroll
       for (int s = 0; s < RS; ++s)
@@ -727,8 +732,8 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
     if (p.bnpart) {   // split form: partials + g; k_bn_bwd forms dz, dgamma, dbeta
       if (!cok) return;
       if (q == 0) {
-        p.bnpart[((int64_t)blockIdx.y * p.K + col) * 2] = sg;
-        p.bnpart[((int64_t)blockIdx.y * p.K + col) * 2 + 1] = sgx;
+        p.bnpart[((int64_t)by * p.K + col) * 2] = sg;
+        p.bnpart[((int64_t)by * p.K + col) * 2 + 1] = sgx;
       }
 #pragma unroll
       for (int s = 0; s < RS; ++s)
@@ -752,6 +757,11 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
       const float dz = p.bn ? p3d_bn_dz(inv, fm, g[s][r], sg, xh[s][r], sgx) : g[s][r];
       p.dz[p3d_pk(row, col, ngK)] = dz;
     }
+}
+
+template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
+__global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
+  p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
 // =====================================================================================
@@ -827,6 +837,7 @@ struct WgradArgs {
   // ... and to the previous layer's BN gamma / beta ([K]; flat offsets goff / btoff), whose
   // gradients k_bn_bwd wrote to gflat just before (all readers of gamma/beta are done)
   int bn_adam; const float* gflat; int64_t goff, btoff;
+  const float* alpha_dev;         // if set: the step's Adam alpha, formed by an earlier launch
 };
 
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
@@ -892,7 +903,8 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     __syncthreads();
   }
   float alpha = 0.f;
-  if (p.adam) alpha = p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
+  if (p.adam)
+    alpha = p.alpha_dev ? *p.alpha_dev : p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
   if (do_db) {
     dbp[w][lane] = dbs;
     __syncthreads();
@@ -961,10 +973,11 @@ struct WgradMulti {
   int begin[P3D_WG_MULTI + 1];   // workgroup prefix over layers
   int gx[P3D_WG_MULTI];          // column tiles of each layer
   int adam; AdamFuse af; float* w; float* m; float* v; const float* gflat;
+  const float* alpha_dev;        // fused Adam: alpha formed by an earlier launch of the step (or null)
+  StepState* advance;            // if set: this launch's workgroup 0 advances the step state at its end
   WgradLayer ly[P3D_WG_MULTI];
 };
-__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
-  const int b = blockIdx.x;
+__device__ __forceinline__ void p3d_wgrad_multi_tile(const WgradMulti& mw, int b) {
   int j = 0;
   while (j + 1 < mw.n && b >= mw.begin[j + 1]) ++j;
   const WgradLayer& l = mw.ly[j];
@@ -975,9 +988,38 @@ __global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
     p.adam = 1; p.af = mw.af; p.w = mw.w; p.m = mw.m; p.v = mw.v; p.woff = l.woff; p.boff = l.boff;
     p.wd = l.wd; p.wf = l.wf;
     p.bn_adam = l.bn_adam; p.gflat = mw.gflat; p.goff = l.goff; p.btoff = l.btoff;
+    p.alpha_dev = mw.alpha_dev;
   }
   const int loc = b - mw.begin[j];
   p3d_wgrad_tile(p, loc % mw.gx[j], loc / mw.gx[j]);
+}
+__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
+  p3d_wgrad_multi_tile(mw, blockIdx.x);
+  // the step's last launch: nothing in it reads the step state (alpha came from alpha_dev),
+  // so one thread may advance it here instead of a k_step_advance launch
+  if (mw.advance && blockIdx.x == 0 && threadIdx.x == 0) {
+    StepState* st = mw.advance;
+    st->beta1_power = st->beta1_power * mw.af.b1;
+    st->beta2_power = st->beta2_power * mw.af.b2;
+    st->global_step = st->global_step + 1;
+  }
+}
+
+// A data-gradient launch carrying the weight-gradient (+ fused Adam) tiles of the layer above:
+// blocks [0, gx*gy) are k_dgrad's tiles of this layer, the rest mw's tiles (256 threads: the
+// upper half of those workgroups exits at once).  The tiles of layer l + 1 ride the dgrad
+// launch of layer l: their dZ is final, W(l + 1) was read by the previous launch, and nothing in
+// this launch reads what they update (this layer's dgrad reads W(l) and layer l - 1's gamma,
+// beta); so the single-GPU step's separate k_wgrad_multi launch shrinks to the first two layers.
+template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
+__global__ __launch_bounds__(64 * WK) void k_dgrad_wg(BwdArgs p, WgradMulti mw, int gx, int gy) {
+  const int b = blockIdx.x, nd = gx * gy;
+  if (b < nd) {
+    p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, b % gx, b / gx, gy);
+    return;
+  }
+  if (threadIdx.x >= 256) return;
+  p3d_wgrad_multi_tile(mw, b - nd);
 }
 
 // =====================================================================================
@@ -1315,6 +1357,11 @@ struct p3d_model {
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
   std::vector<hipEvent_t> gev;   // per-layer gradient-ready events (p3d_grad_events)
   int wgrad_multi = 1;           // all layers' dW in one k_wgrad_multi launch (env P3D_WGRAD_MULTI)
+  int wgrad_attach = 0;          // fused train step: layer l + 1's dW + Adam tiles ride layer l's dgrad launch
+                                 // (k_dgrad_wg; env P3D_WGRAD_ATTACH=1; bit-identical, measured slower:
+                                 // 129.7 vs 126.3 us per cfg3 step -- the optimizer traffic slows the dgrad)
+  float* alpha_dev = nullptr;    // the step's Adam alpha, formed by the first backward launch
+  bool step_advanced = false;    // set by a backward whose last launch advanced the step state
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
   int serve6 = 1;           // k_serve6 for launches of <= serve6_max_nb steps (env P3D_SERVE6: 0 off, 1 auto, 2 always)
   int serve6_max_nb = 32;   // (env P3D_SERVE6_MAX_NB)
@@ -1371,6 +1418,7 @@ void free_all(p3d_model* m) {
   if (m->serve_sync) (void)hipFree(m->serve_sync);
   if (m->serve_ecg) (void)hipFree(m->serve_ecg);
   if (m->xsync) (void)hipFree(m->xsync);
+  if (m->alpha_dev) (void)hipFree(m->alpha_dev);
 }
 // ---- teardown in any order -------------------------------------------------------------
 // A model's device memory must go while the HIP runtime is alive and nothing still runs on
@@ -1600,6 +1648,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
+  if (const char* ev = getenv("P3D_WGRAD_ATTACH")) m->wgrad_attach = atoi(ev);
+  if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH5")) m->serve_depth5 = atoi(ev);
@@ -2495,6 +2545,13 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (m->fuse_adam) {
     mw.adam = 1; mw.af = *m->fuse_adam; mw.w = m->flat[0]; mw.m = m->flat[2]; mw.v = m->flat[3]; mw.gflat = grads;
   }
+  // fused single-GPU step: Adam's alpha formed once by the first backward launch, so the last
+  // launch (which reads no step state) advances it -- no k_step_advance launch; optionally the
+  // tiles of layer l + 1 ride the dgrad launch of layer l (k_dgrad_wg, P3D_WGRAD_ATTACH=1)
+  const bool fused_tail = multi && m->fuse_adam && m->train_split;
+  const bool attach = fused_tail && m->wgrad_attach;
+  if (fused_tail) mw.alpha_dev = m->alpha_dev;
+  m->step_advanced = false;
   // a layer's weight gradient (+ fused Adam): into the batched launch, or launched now
   auto emit = [&](const WgradArgs& wa) -> int {
     if (!multi) return launch_wgrad(m, wa, st);
@@ -2575,12 +2632,22 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       const bool xchg = pv.bn && use_xchg(m, a.K, a.M) && m->gev.empty();
       if (xchg) { a.xchg = 1; a.xs = xchg_site(m, nl + l - 1); }   // dz, dgamma, dbeta here
       const dim3 grid((a.K + 15) / 16, (a.M + 15) / 16);
+      const bool carry = attach && mw.n > 0 && dz_pk;   // layer l + 1's dW + Adam tiles ride along
+      if (fused_tail && is_out) { a.alpha_out = m->alpha_dev; a.af = *m->fuse_adam; }
       {
-        ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
-        if (dz_pk) go(ps, k_dgrad<1, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
-        else go(ps, k_dgrad<1, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
+        ProfScope ps(m, is_out ? "dgrad_out" : carry ? "dgrad_wgrad" : "dgrad_hidden");
+        if (carry) {
+          const int gx = (int)grid.x, gy = (int)grid.y;
+          go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, dim3((unsigned)(gx * gy + mw.begin[mw.n])), dim3(512), st, a, mw,
+             gx, gy);
+        } else if (dz_pk) {
+          go(ps, k_dgrad<1, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
+        } else {
+          go(ps, k_dgrad<1, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
+        }
       }
       LAUNCH_CHECK("k_dgrad");
+      if (carry) { mw.n = 0; mw.begin[0] = 0; }
       if (pv.bn && !xchg) {
         BnBwdArgs b{};
         b.dz = a.dz; b.z = a.z; b.part = m->bnpart; b.M = a.M; b.K = a.K;
@@ -2615,6 +2682,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     dz_pk = true;
   }
   if (multi && mw.n > 0) {
+    if (fused_tail) { mw.advance = m->dstate; m->step_advanced = true; }   // the step's last launch
     ProfScope ps(m, "wgrad_multi");
     go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
     LAUNCH_CHECK("k_wgrad_multi");
@@ -2703,8 +2771,11 @@ extern "C" int p3d_train_step(p3d_model* m, const float* x, const float* t, int6
   const int rc = p3d_train_fwd_bwd(m, x, t, B, y, keep_prob, seed, 0, loss_dev, stream);
   m->fuse_adam = nullptr;
   if (rc) return rc;
-  k_step_advance<<<1, 1, 0, st>>>(m->dstate, af.b1, af.b2);
-  LAUNCH_CHECK("k_step_advance");
+  if (!m->step_advanced) {   // (the attached form advanced it in its last launch)
+    k_step_advance<<<1, 1, 0, st>>>(m->dstate, af.b1, af.b2);
+    LAUNCH_CHECK("k_step_advance");
+  }
+  m->step_advanced = false;
   return P3D_OK;
 }
 

@@ -316,13 +316,17 @@ def test_predict14_gradients_and_train_steps():
     m.close()
 
 
-@pytest.mark.parametrize("residual,batch_norm", [(True, True), (False, False), (True, False)])
-def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, monkeypatch):
+@pytest.mark.parametrize("residual,batch_norm,attach", [(True, True, "0"), (False, False, "0"), (True, False, "0"),
+                                                       (True, True, "1")])
+def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, attach, monkeypatch):
     """p3d_train_step with Adam inside the gradient kernels (P3D_FUSE_ADAM=1) ==
     p3d_train_fwd_bwd + p3d_adam_step_decay, bit for bit, over 4 steps (weights, slots,
-    moving stats, step)."""
+    moving stats, step).  attach=0 (default): one k_wgrad_multi launch after the backward, which
+    also advances the step state (alpha formed by the first backward launch); attach=1: layer
+    l + 1's weight-gradient + Adam tiles ride layer l's data-gradient launch."""
     import _p3d
     monkeypatch.setenv("P3D_FUSE_ADAM", "1")
+    monkeypatch.setenv("P3D_WGRAD_ATTACH", attach)
     cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=residual, batch_norm=batch_norm)
     st = ref_mlp.init_state(cfg, seed=4, bn_seed=5)
     ms = []
