@@ -1307,6 +1307,13 @@ struct p3d_model {
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
   int bf16_stages = 48;             // hidden bf16 GEMM variant (launch_bf16_layer; env P3D_BF16_STAGES)
+  int bf16_split = 0;               // hidden bf16 layers as k_gemm_bf16s (256 x 128 tiles, K split in two
+                                    // halves that meet in the launch) where M % 256 == 0 (env P3D_BF16_SPLIT=1;
+                                    // measured 43.9 vs 44.6 us in step order, 42.5 vs 39.0 us hot: opt-in)
+  float* bf16s_part = nullptr;      // k_gemm_bf16s upper-half partials [tiles][8][16][64] f32x4
+  unsigned* bf16s_sync = nullptr;   // k_gemm_bf16s per-tile epoch / flag words
+  int64_t bf16s_tiles = 0;          // tiles the two buffers above hold
+  std::string bf16_kname;           // the kernel the last hidden bf16 layer ran (p3d_kernel_name 5)
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
@@ -1417,6 +1424,8 @@ void free_all(p3d_model* m) {
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
   if (m->serve_ecg) (void)hipFree(m->serve_ecg);
+  if (m->bf16s_part) (void)hipFree(m->bf16s_part);
+  if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
 }
@@ -1693,6 +1702,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     }
     m->Mpad128 = (c.max_batch + 127) / 128 * 128;
     if (const char* ev = getenv("P3D_BF16_STAGES")) m->bf16_stages = atoi(ev);
+    if (const char* ev = getenv("P3D_BF16_SPLIT")) m->bf16_split = atoi(ev);
     const int64_t slab = m->Mpad128 * L;  // bf16 elements per activation slab
     if ((e = hipMalloc(&m->wbf, nbf * 2)) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->wbf, 0, nbf * 2)) != hipSuccess) return cleanup(e);
@@ -1983,6 +1993,31 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
   const bool second = (l >= 1 && ((l - 1) % 2 == 1));
   a.res = (c.residual && second) ? m->abf + (int64_t)(l - 2) * slab : nullptr;
   const unsigned grid = (unsigned)((Mp / 128) * (ly.N / 128));
+  if (l > 0 && m->bf16_split && Mp % 256 == 0 && ly.N % 128 == 0 && ly.K % 128 == 0) {
+    const int64_t T = (int64_t)(Mp / 256) * (ly.N / 128);
+    if (T > m->bf16s_tiles) {
+      hipError_t e;
+      if (m->bf16s_part) { (void)hipFree(m->bf16s_part); m->bf16s_part = nullptr; }
+      if (m->bf16s_sync) { (void)hipFree(m->bf16s_sync); m->bf16s_sync = nullptr; }
+      m->bf16s_tiles = 0;
+      if ((e = hipMalloc(&m->bf16s_part, T * 8 * 16 * 1024)) != hipSuccess)
+        return fail(P3D_ERR_HIP, std::string("k_gemm_bf16s: ") + hipGetErrorString(e));
+      if ((e = hipMalloc(&m->bf16s_sync, T * 64 * sizeof(unsigned))) != hipSuccess)
+        return fail(P3D_ERR_HIP, std::string("k_gemm_bf16s: ") + hipGetErrorString(e));
+      // zero epochs and flags (stream-ordered before the first launch that uses them)
+      if ((e = hipMemsetAsync(m->bf16s_sync, 0, T * 64 * sizeof(unsigned), st)) != hipSuccess)
+        return fail(P3D_ERR_HIP, std::string("k_gemm_bf16s: ") + hipGetErrorString(e));
+      m->bf16s_tiles = T;
+    }
+    GemmBf16SplitArgs sa{};
+    sa.g = a; sa.part = m->bf16s_part; sa.sync = m->bf16s_sync; sa.err = m->xerr;
+    ProfScope ps(m, "bf16_hidden");
+    m->bf16_kname = "k_gemm_bf16s<3>";
+    go(ps, k_gemm_bf16s<3>, dim3((unsigned)(2 * T)), dim3(512), st, sa);
+    LAUNCH_CHECK("k_gemm_bf16s");
+    return P3D_OK;
+  }
+  if (l > 0) m->bf16_kname = m->bf16_stages == 48 ? "k_gemm_bf16p<64, 4, 8, false>" : "k_gemm_bf16p";
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
     if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
@@ -2907,6 +2942,8 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     n = m->train_split ? "k_fwd<1, 8, 8, 2, true, true, 1>" : "k_fwd<4, 8, 8, 2, true, true, 1>";
   } else if (what == 4) {
     n = "k_gemv<4, 16, 4>";   // inference hidden layer at B <= gemv_maxb
+  } else if (what == 5) {
+    n = m->bf16_kname;        // the kernel the last hidden bf16 layer ran
   } else {
     return fail(P3D_ERR_ARG, "p3d_kernel_name: unknown kernel selector");
   }

@@ -762,9 +762,10 @@ def bench_stress(args, rank, world, steps=None, warmup=None):
     iso_us = profile_kernels(model, lambda: lay(50))["bf16_hidden"][1]
     flop = 2.0 * Bs * Ls * Ls
     achieved = flop / (avg_us * 1e-6) / 1e12
+    kname = kernel_name(model, 5)
     roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic("k_gemm_bf16p<64, 4, 8, false>", {"mode": "stress", "batch": Bs}),
-            "kernel": "k_gemm_bf16p<64, 4, 8, false> (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": _committed_traffic(kname, {"mode": "stress", "batch": Bs}),
+            "kernel": kname + " (hidden [1024,4096]x[4096,4096] bf16 MFMA 16x16x32 + BN/ReLU/residual)",
             "flop_per_launch": int(flop), "avg_us": round(avg_us, 3), "launches_timed": reps,
             "isolated_avg_us": round(iso_us, 3)}
     model.close()
