@@ -1,10 +1,12 @@
 // launch_probe.hip -- host enqueue cost of a kernel launch vs the size of its argument struct
 // (the k_serve6 launch passes ~1 KB: ServeArgs with 16 ServeLayer records).  Prints the median
 // host time of one <<<>>> enqueue, and of enqueue + hipStreamSynchronize, for 64 B, 256 B and
-// 1 KB argument structs, 256 x 256 threads, each kernel reading one word of its arguments.
+// 1 KB argument structs, 256 x 256 threads, each kernel reading one word of its arguments; the
+// round trip waits with hipDeviceSynchronize (torch.cuda.synchronize), under each schedule flag.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <cstdio>
 #include <vector>
 
@@ -32,7 +34,7 @@ static void run(hipStream_t st, int* out) {
     const double t0 = now_us();
     k_probe<BYTES><<<256, 256, 0, st>>>(a, out);
     const double t1 = now_us();
-    (void)hipStreamSynchronize(st);
+    (void)hipDeviceSynchronize();
     const double t2 = now_us();
     enq.push_back(t1 - t0);
     rt.push_back(t2 - t0);
@@ -43,7 +45,16 @@ static void run(hipStream_t st, int* out) {
          rt[100]);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1]: device schedule flag set before the runtime initialises the device
+  // (auto = HIP's default, spin = hipDeviceScheduleSpin, yield, block = BlockingSync)
+  const char* mode = argc > 1 ? argv[1] : "auto";
+  unsigned fl = hipDeviceScheduleAuto;
+  if (!strcmp(mode, "spin")) fl = hipDeviceScheduleSpin;
+  else if (!strcmp(mode, "yield")) fl = hipDeviceScheduleYield;
+  else if (!strcmp(mode, "block")) fl = hipDeviceScheduleBlockingSync;
+  if (hipSetDeviceFlags(fl) != hipSuccess) printf("{\"warning\": \"hipSetDeviceFlags failed\"}\n");
+  printf("{\"schedule\": \"%s\"}\n", mode);
   hipStream_t st;
   int* out;
   (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
