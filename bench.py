@@ -186,7 +186,7 @@ def _committed_traffic_avg(symbol, config):
     return None
 
 
-def cpu_baseline(mode, seconds=12.0):
+def cpu_baseline(mode, seconds=12.0, Lc=L, Nc=NBLK):
     """numpy fp32 restatement of the TF1 path (oracle/ref_mlp.py) on this host's cores."""
     from oracle import ref_mlp
     try:
@@ -194,7 +194,7 @@ def cpu_baseline(mode, seconds=12.0):
         threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
     except Exception:
         threads = 1
-    cfg = ref_mlp.Cfg(linear_size=L, num_layers=NBLK, residual=True, batch_norm=True)
+    cfg = ref_mlp.Cfg(linear_size=Lc, num_layers=Nc, residual=True, batch_norm=True)
     st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
     rng = np.random.default_rng(0)
     x = rng.standard_normal((BATCH, IN)).astype(np.float32)
@@ -209,8 +209,8 @@ def cpu_baseline(mode, seconds=12.0):
         n += 1
     dt = time.perf_counter() - t0
     out = {"value": round(n * BATCH / dt, 1), "unit": "poses/s", "cores": int(threads), "kind": "port",
-           "sample": "%d %s batches of 64 (cfg2 model, fp32 numpy restatement of src/linear_model.py), %.1f s"
-                     % (n, "train-step" if mode == "train" else "inference", dt)}
+           "sample": "%d %s batches of 64 (L=%d, %d blocks, fp32 numpy restatement of src/linear_model.py), %.1f s"
+                     % (n, "train-step" if mode == "train" else "inference", Lc, Nc, dt)}
     try:   # the same restatement on one core (SURVEY 8d asks for both)
         from threadpoolctl import threadpool_limits
         with threadpool_limits(limits=1):
@@ -223,6 +223,42 @@ def cpu_baseline(mode, seconds=12.0):
                            "sample": "%d batches, %.1f s" % (n1, dt1)}
     except Exception as exc:
         out["one_core"] = {"error": repr(exc)[:200]}
+    return out
+
+
+def bench_cfg1(seconds=3.0, steps=400):
+    """BASELINE.json configs[0]: L=256, 1 residual block, batch 64, fp32 -- the reference's
+    CPU-runnable plumbing case: the numpy restatement of the TF1 path on the host (inference and
+    train step) beside the HIP path on the same shapes (per-step kernel chain, one stream,
+    eager launches; BN-train layers one launch each)."""
+    import torch
+    import linear_model
+    out = {"workload": "cfg1: L=256, 1 residual block, BN, batch 64, fp32 (keep 1.0 inference, keep 0.5 train)",
+           "cpu": {"infer": cpu_baseline("infer", seconds, 256, 1), "train": cpu_baseline("train", seconds, 256, 1)}}
+    m = linear_model.LinearModel(256, 1, True, True, False, BATCH, 1e-3, "/tmp/p3d_bench", seed=5, max_batch=BATCH,
+                                 data_parallel=False)
+    rng = np.random.default_rng(7)
+    X = torch.from_numpy(rng.standard_normal((steps, BATCH, IN)).astype(np.float32)).cuda()
+    T = torch.from_numpy(rng.standard_normal((steps, BATCH, OUT)).astype(np.float32)).cuda()
+    Y = torch.empty((BATCH, OUT), dtype=torch.float32, device="cuda")
+    gpu = {}
+    for mode in ("infer", "train"):
+        def run(k):
+            for i in range(k):
+                if mode == "infer":
+                    m.forward_device(X[i], False, 1.0, out=Y)
+                else:
+                    m.train_step_device(X[i], T[i], 0.5, out=Y)
+        run(20)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        gpu[mode] = {"value": round(steps * BATCH / dt, 1), "unit": "poses/s", "ms_per_step": round(1e3 * dt / steps, 5),
+                     "note": "%d eager steps, one stream" % steps}
+    m.close()
+    out["gpu"] = gpu
     return out
 
 
@@ -1025,6 +1061,7 @@ def main():
             cpu = None
         else:
             cpu = cpu_baseline(args.mode, args.cpu_seconds)
+        cfg1 = bench_cfg1() if (args.mode == "infer" and not args.no_cpu and world == 1) else None
         metric = {"stress": "poses/sec at batch 1024 (cfg5 bf16 stress)",
                   "eval": "frames/sec, evaluateActionWise MPJPE sweep (cfg4)",
                   "data": "camera-poses/sec, H3.6M train-set preprocessing (float64)"}.get(
@@ -1055,6 +1092,8 @@ def main():
             line["data_pipeline"] = data
         if stress is not None:
             line["stress"] = stress
+        if cfg1 is not None:
+            line["cfg1"] = cfg1
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
