@@ -1803,6 +1803,16 @@ extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
   return refresh_derived(m, (hipStream_t)stream);
 }
 
+// Device-side parameter changes the host did not see issued (a replayed graph of training
+// steps: the kernels ran, this library's host code did not): tables derived from the
+// parameters on the host's schedule -- k_serve6's epilogue constants -- are re-formed at their
+// next use.  No device work.
+extern "C" int p3d_params_changed(p3d_model* m) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  m->serve_ec_dirty = true;
+  return P3D_OK;
+}
+
 // ---- launch helpers ------------------------------------------------------------------
 // Inference: 16x16 output tile per workgroup (grid 64 x 4 = 256 WGs for the 1024-wide
 // layers at B = 64), 8 (or 16) waves split the contraction (every operand load of a wave

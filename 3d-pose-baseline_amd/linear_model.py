@@ -598,8 +598,12 @@ class LinearModel(object):
 
     # ---- step() from host arrays: the session.run path with one H2D, one D2H, one sync ------
     def _host_step_state(self, training, B, keep):
-        """Pinned staging buffers (and, for evaluation, a HIP graph of H2D copy + forward +
-        MSE + D2H copy) for one (mode, batch, keep_prob), cached."""
+        """Pinned staging buffers and a HIP graph of H2D copy + forward + MSE [+ backward +
+        Adam] + D2H copy for one (mode, batch, keep_prob), cached.  Training replays the
+        captured step too (single GPU; the dropout counter, lr decay and Adam beta powers come
+        from the device step state, so every replay is the next step): one graph launch in place
+        of a dozen kernel launches from the host per session.run.  Data-parallel training (its
+        all-reduce) and P3D_STEP_GRAPH=0 run the step eagerly."""
         torch = self.torch
         key = (training, B, keep, self.lr0, self.seed)
         st = self._host_steps.get(key)
@@ -635,6 +639,21 @@ class LinearModel(object):
             with torch.cuda.graph(g, stream=side):
                 body()
             st["graph"] = g
+        elif not self.data_parallel and os.environ.get("P3D_STEP_GRAPH", "1") != "0":
+            def body():
+                st["dx"].copy_(st["hx"], non_blocking=True)
+                st["dt"].copy_(st["ht"], non_blocking=True)
+                loss, _ = self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"])
+                st["hy"].copy_(st["dy"], non_blocking=True)
+                st["hl"].copy_(loss, non_blocking=True)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            # captured, not run (a training step has side effects): no eager warm-up
+            with torch.cuda.graph(g, stream=side):
+                body()
+            self._step_host -= 1            # the capture issued no step
+            st["graph"] = g
         self._host_steps[key] = st
         return st
 
@@ -655,7 +674,12 @@ class LinearModel(object):
         np.copyto(st["ht_np"], t, casting="unsafe")
         stream = self.torch.cuda.current_stream(self.device)
         if st["graph"] is not None:
+            if training:
+                lr = exponential_decay(self.lr0, self._step_host)
             st["graph"].replay()
+            if training:
+                self._step_host += 1
+                check(lib().p3d_params_changed(self._h), "p3d_params_changed")
         else:
             lr = exponential_decay(self.lr0, self._step_host)
             st["dx"].copy_(st["hx"], non_blocking=True)

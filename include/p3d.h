@@ -86,6 +86,13 @@ int p3d_flat_ptr(p3d_model* m, int32_t which /*0 params,1 grads,2 adam_m,3 adam_
  * p3d_flat_ptr (refreshes derived device layouts, e.g. transposed weights). */
 int p3d_params_updated(p3d_model* m, void* stream);
 
+/* The parameters changed on the device without this library's host code issuing the change
+ * (e.g. a replayed HIP graph of training steps, LinearModel.step's cached training graph):
+ * host-scheduled derived tables (k_serve6's epilogue constants) are re-formed at their next
+ * use.  Host-only, no device work.  Replaces nothing in the reference (TF re-reads variables
+ * on every session.run). */
+int p3d_params_changed(p3d_model* m);
+
 /* Forward pass: y[B, output_size] = MLP(x[B, input_size]).
  *   training=0: BN uses moving statistics (isTraining=False, linear_model.py:239-245);
  *               at B <= 4 (env P3D_GEMV_MAXB) every layer is a weight-streaming GEMV kernel

@@ -604,3 +604,27 @@ def test_bf16_split_k_matches_single_pass(L, N, B, monkeypatch):
     err = np.abs(ys["1"] - ys["0"])
     tmax, tmean = (1e-2, 1e-3) if L >= 1024 else (1e-3, 1e-5)
     assert err.max() <= tmax * scale and err.mean() <= tmean * scale, (err.max(), err.mean(), scale)
+
+
+def test_step_training_graph_bit_identical_to_eager(monkeypatch):
+    """LinearModel.step(isTraining=True) from numpy replays a cached HIP graph of the whole
+    training step (H2D, forward, MSE, backward, fused Adam, D2H); the same steps issued eagerly
+    (P3D_STEP_GRAPH=0) give the same bits: outputs, losses, weights, Adam slots, step state,
+    learning-rate summaries."""
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=True, batch_norm=True)
+    rng = np.random.default_rng(77)
+    batches = [(rng.standard_normal((64, 32)), rng.standard_normal((64, 48))) for _ in range(6)]
+    runs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("P3D_STEP_GRAPH", mode)
+        st, m = make(cfg, lr=1e-3)
+        res = [m.step(None, x, t, 0.5, isTraining=True) for x, t in batches]
+        runs[mode] = (res, m.get_state(), m.get_step(), m._step_host)
+        m.close()
+    (ra, sa, ga, ha), (rb, sb, gb, hb) = runs["1"], runs["0"]
+    assert ga == gb and ha == hb == 6
+    for (la, _, lra, oa), (lb, _, lrb, ob) in zip(ra, rb):
+        assert la == lb and lra.value == lrb.value
+        np.testing.assert_array_equal(oa, ob)
+    for k in sa:
+        np.testing.assert_array_equal(np.asarray(sa[k]), np.asarray(sb[k]), err_msg=k)

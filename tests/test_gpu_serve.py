@@ -267,6 +267,13 @@ def test_serve6_constants_follow_parameter_updates():
     m.serve_check()
     assert not torch.equal(y0, y1)
     close(y1.cpu().numpy(), m.forward_device(xd, False, 1.0).cpu().numpy(), atol=5e-5, rtol=5e-5)
+    # a second step() replays the cached training graph (no host code of the library runs
+    # for it; p3d_params_changed marks the table stale)
+    m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 0.5, isTraining=True)
+    y1b = m.serve_device(xd).clone()
+    m.serve_check()
+    assert not torch.equal(y1, y1b)
+    close(y1b.cpu().numpy(), m.forward_device(xd, False, 1.0).cpu().numpy(), atol=5e-5, rtol=5e-5)
     st2 = ref_mlp.init_state(cfg, seed=9, bn_seed=10)
     m.set_weights({**st2.params, **st2.moving})
     y2 = m.serve_device(xd)
