@@ -1367,6 +1367,10 @@ struct p3d_model {
   int wgrad_attach = 0;          // fused train step: layer l + 1's dW + Adam tiles ride layer l's dgrad launch
                                  // (k_dgrad_wg; env P3D_WGRAD_ATTACH=1; bit-identical, measured slower:
                                  // 129.7 vs 126.3 us per cfg3 step -- the optimizer traffic slows the dgrad)
+  int wgrad_side = 0;            // fused train step: layer l's dW + Adam (l >= 1) on the side stream as soon
+                                 // as dgrad(l) is done, overlapping the rest of the dgrad chain (env P3D_WGRAD_SIDE)
+  hipStream_t side = nullptr;    // that side stream (non-blocking; forked from / joined to the caller's stream)
+  std::vector<hipEvent_t> sev;   // fork events (one per layer) + the join event (last)
   float* alpha_dev = nullptr;    // the step's Adam alpha, formed by the first backward launch
   bool step_advanced = false;    // set by a backward whose last launch advanced the step state
   int serve_upm = 2;        // k_serve5 units per contraction (env P3D_SERVE_UPM: 1, 2 with SPLIT >= 2, 4 with SPLIT = 4)
@@ -1428,6 +1432,10 @@ void free_all(p3d_model* m) {
   if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
+  for (hipEvent_t e : m->sev) (void)hipEventDestroy(e);
+  m->sev.clear();
+  if (m->side) (void)hipStreamDestroy(m->side);
+  m->side = nullptr;
 }
 // ---- teardown in any order -------------------------------------------------------------
 // A model's device memory must go while the HIP runtime is alive and nothing still runs on
@@ -1659,6 +1667,13 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_ATTACH")) m->wgrad_attach = atoi(ev);
   if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
+  if (const char* ev = getenv("P3D_WGRAD_SIDE")) m->wgrad_side = atoi(ev);
+  if (m->wgrad_side) {   // created here, never while a caller captures a graph
+    if ((e = hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking)) != hipSuccess) return cleanup(e);
+    m->sev.assign(nl + 1, nullptr);
+    for (hipEvent_t& se : m->sev)
+      if ((e = hipEventCreateWithFlags(&se, hipEventDisableTiming)) != hipSuccess) return cleanup(e);
+  }
   if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH")) m->serve_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_DEPTH5")) m->serve_depth5 = atoi(ev);
@@ -2598,6 +2613,36 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (fused_tail) mw.alpha_dev = m->alpha_dev;
   m->step_advanced = false;
   // a layer's weight gradient (+ fused Adam): into the batched launch, or launched now
+  // fused single-GPU step, side form: once dgrad(l) has read W(l) and formed layer l - 1's
+  // dgamma / dbeta, nothing later in the backward reads what dW + Adam(l) reads or writes (the
+  // next dgrads read W(l - 1) and layer l - 2's BN; the dropout counter is advanced only by the
+  // step's last launch, after the join), so layer l's tiles run on the side stream, overlapping
+  // dgrad(l - 1) .. dgrad(1).  Layer 0's tiles stay on the caller's stream with the step advance;
+  // the side stream is joined back before the backward returns (graph capture: fork / join).
+  const bool side = fused_tail && !attach && m->wgrad_side && m->side && (int)m->sev.size() == nl + 1;
+  bool side_used = false;
+  auto emit_to = [&](WgradMulti& t, const WgradArgs& wa) {
+    WgradLayer& w = t.ly[t.n];
+    w.X = wa.X; w.dZ = wa.dZ; w.dW = wa.dW; w.db = wa.db; w.ldx = wa.ldx; w.ldz = wa.ldz;
+    w.xpk = wa.xpk; w.zpk = wa.zpk; w.M = wa.M; w.K = wa.K; w.N = wa.N;
+    w.bn_adam = wa.bn_adam; w.woff = wa.woff; w.boff = wa.boff; w.goff = wa.goff; w.btoff = wa.btoff;
+    w.wd = wa.wd; w.wf = wa.wf;
+    t.gx[t.n] = (wa.N + 63) / 64;
+    t.begin[t.n + 1] = t.begin[t.n] + t.gx[t.n] * ((wa.K + 63) / 64);
+    ++t.n;
+  };
+  auto emit_side = [&](const WgradArgs& wa, int l) -> int {
+    WgradMulti one = mw;   // the Adam fields and alpha_dev, no layers yet
+    one.n = 0; one.begin[0] = 0; one.advance = nullptr;
+    emit_to(one, wa);
+    HIP_TRY(hipEventRecord(m->sev[l], st));
+    HIP_TRY(hipStreamWaitEvent(m->side, m->sev[l], 0));
+    ProfScope ps(m, "wgrad_side");
+    go(ps, k_wgrad_multi, dim3(one.begin[1]), dim3(256), m->side, one);
+    LAUNCH_CHECK("k_wgrad_multi (side)");
+    side_used = true;
+    return P3D_OK;
+  };
   auto emit = [&](const WgradArgs& wa) -> int {
     if (!multi) return launch_wgrad(m, wa, st);
     WgradLayer& w = mw.ly[mw.n];
@@ -2718,7 +2763,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     }
     if (a.draw) { dres_next = a.draw; dsel ^= 1; }
     if (fuse) {
-      int rc = emit(wa);
+      int rc = side ? emit_side(wa, l) : emit(wa);
       if (rc) return rc;
     }
     // layer l's W and b (wgrad above) and its gamma/beta (bn_bwd of iteration l + 1) are final
@@ -2728,9 +2773,13 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   }
   if (multi && mw.n > 0) {
     if (fused_tail) { mw.advance = m->dstate; m->step_advanced = true; }   // the step's last launch
-    ProfScope ps(m, "wgrad_multi");
+    ProfScope ps(m, side_used ? "wgrad_tail" : "wgrad_multi");
     go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
     LAUNCH_CHECK("k_wgrad_multi");
+  }
+  if (side_used) {   // join: the caller's stream (and a graph being captured on it) waits for the side
+    HIP_TRY(hipEventRecord(m->sev[nl], m->side));
+    HIP_TRY(hipStreamWaitEvent(st, m->sev[nl], 0));
   }
   if (c.max_norm) {
     // G (dL/dW_eff) -> dL/dW through clip_by_norm

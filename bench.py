@@ -556,16 +556,28 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         shapes = [(IN, L)] + [(L, L)] * (2 * NBLK) + [(L, OUT)]
         byts = sum(4 * (BATCH * K + BATCH * N) + 4 * 8 * K * N + 4 * 6 * N for K, N in shapes)
         byts += 4 * 12 * L * (2 * NBLK + 1)          # gamma, beta of every BN layer
-        multi = "wgrad_multi" in prof                # all layers in one launch (default)
-        cnt, avg_us, _, _ = prof["wgrad_multi" if multi else "wgrad"]
-        per_step = 1 if multi else len(shapes)
+        if "wgrad_side" in prof:
+            # default side form: layer l's dW + Adam (l >= 1) launched on the model's side stream
+            # right after dgrad(l), overlapping the rest of the dgrad chain; layer 0's tiles
+            # (K = 32) ride the step's last launch ("wgrad_tail").  Roofline over the side
+            # launches: bytes of layers 1.. ÷ (launches per step x their average duration).
+            cnt, avg_us, _, _ = prof["wgrad_side"]
+            per_step = len(shapes) - 1
+            K0, N0 = shapes[0]
+            byts = byts - (4 * (BATCH * K0 + BATCH * N0) + 4 * 8 * K0 * N0 + 4 * 6 * N0)
+            kname = ("k_wgrad_multi on the side stream (fused TF1 Adam + Wf/Wd re-pack), one launch per layer "
+                     "for layers 1..%d, each overlapping the remaining dgrad chain" % per_step)
+            traffic = None
+        else:
+            multi = "wgrad_multi" in prof            # all layers in one launch
+            cnt, avg_us, _, _ = prof["wgrad_multi" if multi else "wgrad"]
+            per_step = 1 if multi else len(shapes)
+            kname = ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
+                     if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step)
+            traffic = _committed_traffic("k_wgrad_multi" if multi else "k_wgrad", {"mode": "train", "batch": BATCH})
         achieved = byts / (per_step * avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": _committed_traffic("k_wgrad_multi" if multi else "k_wgrad",
-                                              {"mode": "train", "batch": BATCH}),
-                "kernel": ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
-                           if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "bytes_per_step": int(byts), "avg_us": round(avg_us, 3), "launches_timed": cnt}
     roof["event_pair_avg_us"] = {k: round(v[1], 3) for k, v in prof.items()}
     model.close()

@@ -316,17 +316,21 @@ def test_predict14_gradients_and_train_steps():
     m.close()
 
 
-@pytest.mark.parametrize("residual,batch_norm,attach", [(True, True, "0"), (False, False, "0"), (True, False, "0"),
-                                                       (True, True, "1")])
-def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, attach, monkeypatch):
+@pytest.mark.parametrize("residual,batch_norm,attach,side", [(True, True, "0", "1"), (False, False, "0", "1"),
+                                                            (True, False, "0", "1"), (True, True, "0", "0"),
+                                                            (False, False, "0", "0"), (True, True, "1", "0")])
+def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, attach, side, monkeypatch):
     """p3d_train_step with Adam inside the gradient kernels (P3D_FUSE_ADAM=1) ==
     p3d_train_fwd_bwd + p3d_adam_step_decay, bit for bit, over 4 steps (weights, slots,
-    moving stats, step).  attach=0 (default): one k_wgrad_multi launch after the backward, which
-    also advances the step state (alpha formed by the first backward launch); attach=1: layer
-    l + 1's weight-gradient + Adam tiles ride layer l's data-gradient launch."""
+    moving stats, step).  side=1 (default): layer l's weight-gradient + Adam tiles (l >= 1) on the
+    model's side stream right after dgrad(l), layer 0's with the step advance on the caller's
+    stream, then a join; side=0: one k_wgrad_multi launch after the backward, which also advances
+    the step state (alpha formed by the first backward launch); attach=1: layer l + 1's
+    weight-gradient + Adam tiles ride layer l's data-gradient launch."""
     import _p3d
     monkeypatch.setenv("P3D_FUSE_ADAM", "1")
     monkeypatch.setenv("P3D_WGRAD_ATTACH", attach)
+    monkeypatch.setenv("P3D_WGRAD_SIDE", side)
     cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=residual, batch_norm=batch_norm)
     st = ref_mlp.init_state(cfg, seed=4, bn_seed=5)
     ms = []
