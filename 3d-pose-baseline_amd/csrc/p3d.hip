@@ -1368,7 +1368,9 @@ struct p3d_model {
                                  // (k_dgrad_wg; env P3D_WGRAD_ATTACH=1; bit-identical, measured slower:
                                  // 129.7 vs 126.3 us per cfg3 step -- the optimizer traffic slows the dgrad)
   int wgrad_side = 0;            // fused train step: layer l's dW + Adam (l >= 1) on the side stream as soon
-                                 // as dgrad(l) is done, overlapping the rest of the dgrad chain (env P3D_WGRAD_SIDE)
+                                 // as dgrad(l) is done, overlapping the rest of the dgrad chain (env P3D_WGRAD_SIDE;
+                                 // bit-identical, measured slower: 197-202 vs 122 us per cfg3 step -- the
+                                 // cross-queue graph edges slow every launch of the step)
   hipStream_t side = nullptr;    // that side stream (non-blocking; forked from / joined to the caller's stream)
   std::vector<hipEvent_t> sev;   // fork events (one per layer) + the join event (last)
   float* alpha_dev = nullptr;    // the step's Adam alpha, formed by the first backward launch
