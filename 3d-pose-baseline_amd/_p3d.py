@@ -50,6 +50,7 @@ SIGNATURES = [
     ("p3d_serve", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("p3d_serve_check", c_int32, [c_void_p]),
     ("p3d_sync_check", c_int32, [c_void_p]),
+    ("p3d_error_flags", c_int32, [c_void_p, POINTER(c_int32), c_int32]),
     ("p3d_mse", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     ("p3d_backward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_adam_step", c_int32, [c_void_p, c_float, c_void_p]),
@@ -67,6 +68,10 @@ SIGNATURES = [
     ("p3d_train_fwd_bwd", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
                                     c_void_p, c_void_p]),
     ("p3d_grad_events", c_int32, [c_void_p, c_int32]),
+    ("p3d_grad_buckets", c_int32, [c_void_p, c_int32, c_void_p]),
+    ("p3d_train_fwd_bwd_lr", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
+                                       c_float, c_float, c_float, c_void_p, c_void_p]),
+    ("p3d_adam_apply", c_int32, [c_void_p, c_void_p]),
     ("p3d_layer_grad_range", c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     ("p3d_stream_wait_grad", c_int32, [c_void_p, c_int32, c_void_p]),
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),

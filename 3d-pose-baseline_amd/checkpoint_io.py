@@ -97,18 +97,24 @@ def read_npy_dump(directory: str):
 
 
 def check_state(model, state):
-    """Reject variables this model does not have and shape mismatches (TF's restore raises
-    NotFoundError / InvalidArgumentError for both)."""
-    known = set(global_order(model.param_table))
-    unknown = sorted(set(state) - known)
-    if unknown:
-        raise ValueError("checkpoint variables not in this model: %s" % ", ".join(unknown[:8]))
+    """TF1 ``Saver.restore`` semantics (the Saver of src/linear_model.py:151 lists every global
+    variable): every variable of the model must be in the checkpoint (TF raises NotFoundError
+    otherwise), variables the model does not have are ignored, a shape mismatch is an error
+    (InvalidArgumentError).  Returns the checkpoint restricted to the model's variables."""
+    names = global_order(model.param_table)
+    missing = [n for n in names if n not in state]
+    if missing:
+        raise ValueError("checkpoint lacks variables of this model: %s" % ", ".join(missing[:8]))
     shapes = model._shapes
-    for name, val in state.items():
+    out = {}
+    for name in names:
+        val = state[name]
         want = shapes.get(name[:-len("/Adam_1")] if name.endswith("/Adam_1") else
                           name[:-len("/Adam")] if name.endswith("/Adam") else name)
         if want is not None and tuple(np.shape(val)) != tuple(want):
             raise ValueError("%s: checkpoint shape %s, model shape %s" % (name, np.shape(val), tuple(want)))
+        out[name] = val
+    return out
 
 
 def import_npy_dump(model, directory: str):

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   uint64_t ctr = p.ctr;
   unsigned xtag = 0;
   if (w == 0) {
-    if (p.bn == 4) xtag = p3d_xchg_tag(p.xs);
+    if (p.bn == 4) xtag = p3d_xchg_tag(p.xs, ct, blockIdx.y, gridDim.y);
     if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     b = p.bias[cc];
     if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
         for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu_x[s]);
       }
       p3d_xchg_get(p.xs, p.N, R, cc, xtag, st, qt);
-      p3d_xchg_done(p.xs, blockIdx.y);
+      p3d_xchg_done(p.xs, ct, blockIdx.y);
       float S = 0.f;
 #pragma unroll
       for (int t = 0; t < P3D_XCHG_MAXR; ++t)
@@ -639,7 +639,7 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
   uint64_t ctr = p.ctr;
   unsigned xtag = 0;
   if (w == 0) {
-    if (p.xchg) xtag = p3d_xchg_tag(p.xs);
+    if (p.xchg) xtag = p3d_xchg_tag(p.xs, bx, by, gy);
     if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     if (p.prev && p.bn) { mean = p.mean[cc]; var = p.var[cc]; gam = p.gamma[cc]; bet = p.beta[cc]; }
 #pragma unroll
@@ -711,7 +711,7 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
       float at[P3D_XCHG_MAXR], bt[P3D_XCHG_MAXR];
       p3d_xchg_put(p.xs, p.K, by, col, q == 0 && cok, sg, sgx, xtag);
       p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt);
-      p3d_xchg_done(p.xs, by);
+      p3d_xchg_done(p.xs, bx, by);
       sg = 0.f;
       sgx = 0.f;
 #pragma unroll
@@ -1048,6 +1048,9 @@ struct AdamArgs {
   float* w; float* m; float* v; const float* g;
   float* wpk;
   StepState* st;
+  const float* alpha_dev;   // if set: the step's alpha, formed by the backward's first launch; block 0
+  StepState* advance;       //   then advances the step state (nothing in the launch reads it) -- no
+                            //   k_step_advance launch behind the optimizer
   float lr_host;        // >= 0: use as lr; < 0: device exponential decay of lr0
   float lr0, decay_steps, decay_rate;
   float b1, b2, eps;
@@ -1061,10 +1064,20 @@ __global__ __launch_bounds__(256) void k_adam_pack(AdamArgs a, AdamTable tb) {
   __shared__ float tile[64][65];
   __shared__ float s_alpha;
   if (threadIdx.x == 0) {
-    const float b1p = a.st->beta1_power, b2p = a.st->beta2_power;
-    float lr = a.lr_host;
-    if (lr < 0.f) lr = a.lr0 * powf(a.decay_rate, (float)a.st->global_step / a.decay_steps);
-    s_alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+    if (a.alpha_dev) {
+      s_alpha = *a.alpha_dev;
+      if (a.advance && blockIdx.x == 0) {
+        StepState* st = a.advance;
+        st->beta1_power = st->beta1_power * a.b1;
+        st->beta2_power = st->beta2_power * a.b2;
+        st->global_step = st->global_step + 1;
+      }
+    } else {
+      const float b1p = a.st->beta1_power, b2p = a.st->beta2_power;
+      float lr = a.lr_host;
+      if (lr < 0.f) lr = a.lr0 * powf(a.decay_rate, (float)a.st->global_step / a.decay_steps);
+      s_alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+    }
   }
   __syncthreads();
   const float alpha = s_alpha, omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2;
@@ -1298,9 +1311,16 @@ struct p3d_model {
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
-  unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) an epoch word (own 128-B line), then
-                              // the error word, then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
-  int* xerr = nullptr;        // set when an in-launch synchronisation timed out (p3d_sync_check)
+  unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
+                              // 128-B line each), then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
+  int64_t xslots_off = 0;     // word offset of the slot arrays in xsync
+  int xchg_delay = 0;         // test hook: late row-tile siblings (env P3D_XCHG_TEST_DELAY, p3d_xchg.h)
+  // error words the kernels write and the host reads without a device round trip (pinned, mapped):
+  // [0] a BN-train exchange / split-K hand-off timed out, [1] a p3d_serve launch failed (1: a spin
+  // ran out, 2: an XCD group smaller than the launch was sized for)
+  int* errw = nullptr;        // host view
+  int* xerr = nullptr;        // device view of errw[0]
+  int* serve_err = nullptr;   // device view of errw[1]
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
   float* aff = nullptr;             // BN-eval affine per BN layer
@@ -1350,19 +1370,22 @@ struct p3d_model {
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
-  unsigned serve_epoch = 0;     // k_serve6 launches so far (sync-word bank = epoch & 1)
-  bool serve_banks_clean = true;   // both banks zero (false after a k_serve5 launch used bank 0)
   float* serve_ecg = nullptr;      // k_serve6 epilogue-constant table (k_serve_prep), [layer][tile][48] + divisors
   bool serve_ec_dirty = true;      // parameters or moving statistics changed since the table was formed
-  unsigned* serve_sync = nullptr;
-  int* serve_err = nullptr;
+  unsigned* serve_sync = nullptr;  // [k_serve6 bank 0 | bank 1 | k_serve5 bank | device epoch word ...]
+  int serve_fault = 0;             // test hook: the census waits for one workgroup more than the grid
+                                   // (env P3D_SERVE_TEST_FAULT): every launch fails its census
   int serve_grid = 0;
   int serve_groups = 0;     // at most this many groups take steps, 0 = all (env P3D_SERVE_GROUPS)
   int serve_depth = 2;      // k_serve register-ring depth (env P3D_SERVE_DEPTH, see launch_serve_k)
   int serve_depth5 = 4;     // k_serve5 register-ring depth (env P3D_SERVE_DEPTH5, see serve5_depth)
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
-  std::vector<hipEvent_t> gev;   // per-layer gradient-ready events (p3d_grad_events)
+  std::vector<hipEvent_t> gev;   // per-bucket gradient-ready events (p3d_grad_buckets / p3d_grad_events)
+  std::vector<int> bucket_lo;    // lowest layer of each bucket, buckets in backward order (layers hi..lo)
+  const AdamFuse* alpha_af = nullptr;  // set during p3d_train_fwd_bwd_lr: the backward forms the step's alpha
+  AdamFuse dp_af{};              // hyper-parameters of the last p3d_train_fwd_bwd_lr (p3d_adam_apply)
+  bool alpha_ready = false;      // the last backward formed alpha_dev (p3d_adam_apply reads it)
   int wgrad_multi = 1;           // all layers' dW in one k_wgrad_multi launch (env P3D_WGRAD_MULTI)
   int wgrad_attach = 0;          // fused train step: layer l + 1's dW + Adam tiles ride layer l's dgrad launch
                                  // (k_dgrad_wg; env P3D_WGRAD_ATTACH=1; bit-identical, measured slower:
@@ -1433,6 +1456,7 @@ void free_all(p3d_model* m) {
   if (m->bf16s_part) (void)hipFree(m->bf16s_part);
   if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
+  if (m->errw) (void)hipHostFree(m->errw);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
   for (hipEvent_t e : m->sev) (void)hipEventDestroy(e);
   m->sev.clear();
@@ -1660,11 +1684,20 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     if ((e = hipGetDevice(&dev)) != hipSuccess) return cleanup(e);
     if ((e = hipDeviceGetAttribute(&m->num_cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return cleanup(e);
-    const int64_t nx = (int64_t)(2 * nl + 1) * 32 + (int64_t)2 * nl * P3D_XCHG_MAXR * L * 4;
+    m->xslots_off = (int64_t)2 * nl * (L / 16) * P3D_XCHG_EPOCH_STRIDE;
+    const int64_t nx = m->xslots_off + (int64_t)2 * nl * P3D_XCHG_MAXR * L * 4;
     if ((e = hipMalloc(&m->xsync, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->xsync, 0, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
-    m->xerr = (int*)(m->xsync + 2 * nl * 32);
+    if ((e = hipHostMalloc((void**)&m->errw, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+      return cleanup(e);
+    memset(m->errw, 0, 64 * sizeof(int));
+    int* dv = nullptr;
+    if ((e = hipHostGetDevicePointer((void**)&dv, m->errw, 0)) != hipSuccess) return cleanup(e);
+    m->xerr = dv;
+    m->serve_err = dv + 1;
   }
+  if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_TEST_FAULT")) m->serve_fault = atoi(ev);
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_ATTACH")) m->wgrad_attach = atoi(ev);
@@ -1901,10 +1934,13 @@ static bool use_xchg(const p3d_model* m, int N, int M) {
 }
 static XchgSite xchg_site(const p3d_model* m, int slot) {
   const int nl = (int)m->layers.size();
+  const int L = m->cfg.linear_size;
   XchgSite x;
-  x.epoch = m->xsync + (int64_t)slot * 32;
-  x.slots = (float*)(m->xsync + (int64_t)(2 * nl + 1) * 32) + (int64_t)slot * P3D_XCHG_MAXR * m->cfg.linear_size * 4;
+  x.epoch = m->xsync + (int64_t)slot * (L / 16) * P3D_XCHG_EPOCH_STRIDE;
+  x.slots = (float*)(m->xsync + m->xslots_off) + (int64_t)slot * P3D_XCHG_MAXR * L * 4;
   x.err = m->xerr;
+  x.delay = m->xchg_delay;
+  (void)nl;
   return x;
 }
 
@@ -2388,6 +2424,11 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     return fail(P3D_ERR_ARG, "p3d_serve: needs linear_size % 128 == 0, input/output size <= 64, <= 7 blocks");
   if (!aligned16(x)) return fail(P3D_ERR_ARG, "p3d_serve: x must be 16-byte aligned");
   if ((B + 63) / 64 > 0x7fffffff) return fail(P3D_ERR_ARG, "p3d_serve: too many rows");
+  // an earlier launch failed and nobody has collected the error (p3d_serve_check): refuse, so a
+  // caller never keeps receiving rows of a launch whose workgroups could not synchronise
+  if (m->errw && m->errw[1])
+    return fail(P3D_ERR_HIP, "p3d_serve: an earlier launch failed (not all workgroups resident); p3d_serve_check "
+                             "reports and clears it");
   hipStream_t st = (hipStream_t)stream;
   const int L = c.linear_size, U = L / 32, NDT = (c.output_size + 15) / 16;
   const int64_t slab = (int64_t)64 * L, PT = (int64_t)4 * NDT * 256;
@@ -2404,13 +2445,12 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     if ((e = hipMemset(m->serve_buf, 0, nbuf * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    // [bank 0 | bank 1 | error word]: k_serve5 uses bank 0 (zeroed before each launch),
-    // k_serve6 alternates the banks (p3d_serve6.h)
-    if ((e = hipMalloc(&m->serve_sync, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+    // [bank 0 | bank 1 | k_serve5 bank | epoch word]: k_serve6 alternates banks 0 / 1 by the
+    // device epoch word (p3d_serve6.h), k_serve5 uses bank 2 (zeroed before each of its launches)
+    if ((e = hipMalloc(&m->serve_sync, P3D_SERVE_SYNC_ALL * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    if ((e = hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
+    if ((e = hipMemset(m->serve_sync, 0, P3D_SERVE_SYNC_ALL * sizeof(unsigned))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    m->serve_err = (int*)(m->serve_sync + 2 * P3D_SERVE_SYNC_WORDS);
     const int64_t necg = (int64_t)(2 * c.num_layers + 2) * (L / 16) * 48 + 64;
     if ((e = hipMalloc(&m->serve_ecg, necg * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
@@ -2422,6 +2462,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   a.bn = c.batch_norm; a.residual = c.residual; a.eps = c.bn_eps;
   a.act = m->serve_buf; a.part = m->serve_buf + P3D_SERVE_GROUPS * 3 * slab;
   a.sync = m->serve_sync; a.err = m->serve_err;
+  a.epoch = m->serve_sync + 3 * P3D_SERVE_SYNC_WORDS;
+  a.census_extra = m->serve_fault ? 1 : 0;
   a.max_groups = m->serve_groups;
   for (size_t l = 0; l < m->layers.size(); ++l) {
     const Layer& ly = m->layers[l];
@@ -2442,32 +2484,28 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
   }
   a.ecg = m->serve_ecg;
-  if (use6 && m->serve_ec_dirty) {
+  // a HIP graph being captured replays this call with whatever parameters it then finds: the
+  // epilogue-constant table is formed inside the graph (one small launch per replay), not
+  // decided once at capture time
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if ((e = hipStreamIsCapturing(st, &cap)) != hipSuccess)
+    return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (use6 && (m->serve_ec_dirty || capturing)) {
     // the epilogue-constant table, formed once per parameter version (refresh_derived, a
     // training forward and every Adam step mark it stale): steady-state calls are one launch
-    const int nl = 2 * c.num_layers + 1, nthreads = std::max(nl * L, (int)P3D_SERVE_SYNC_WORDS);
-    ServeArgs pa = a;
-    pa.sync = m->serve_sync + (m->serve_epoch & 1u) * P3D_SERVE_SYNC_WORDS;   // the bank this launch uses: zero
-    k_serve_prep<<<(unsigned)((nthreads + 255) / 256), 256, 0, st>>>(pa, m->serve_ecg);
+    const int nl = 2 * c.num_layers + 1;
+    k_serve_prep<<<(unsigned)((nl * L + 255) / 256), 256, 0, st>>>(a, m->serve_ecg);
     LAUNCH_CHECK("k_serve_prep");
-    m->serve_ec_dirty = false;
+    if (!capturing) m->serve_ec_dirty = false;
   }
-  if (use6) {
-    // no memset in front: this launch's bank was zeroed by the previous k_serve6 launch (or at
-    // allocation); after a k_serve5 launch (bank 0) both banks are zeroed once
-    if (!m->serve_banks_clean) {
-      if ((e = hipMemsetAsync(m->serve_sync, 0, 2 * P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
-        return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-      m->serve_banks_clean = true;
-    }
-    const unsigned bank = m->serve_epoch++ & 1u;
-    a.sync = m->serve_sync + bank * P3D_SERVE_SYNC_WORDS;
-    a.sync_next = m->serve_sync + (bank ^ 1u) * P3D_SERVE_SYNC_WORDS;
-  } else {
-    if ((e = hipMemsetAsync(m->serve_sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
+  if (!use6) {   // k_serve5: its own bank, zeroed in front of every launch
+    a.sync = m->serve_sync + 2 * P3D_SERVE_SYNC_WORDS;
+    if ((e = hipMemsetAsync(a.sync, 0, P3D_SERVE_SYNC_WORDS * sizeof(unsigned), st)) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
-    m->serve_banks_clean = false;
   }
+  // (k_serve6 picks its bank from the device epoch word: no memset in front, graph replays
+  // alternate the banks by themselves)
   if (use6) {
     const int T = L / 16;
     const int ncm = plan.ncm;
@@ -2491,33 +2529,55 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   return P3D_OK;
 }
 
+static const char* serve_err_text(int v) {
+  return v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
+                : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident); the "
+                  "launch's rows hold NaN where its census failed";
+}
+
+// Reported once: the word and the sync words are cleared, so later launches are judged on their own.
+static int serve_report(p3d_model* m, int v) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess && m->serve_sync) e = hipMemset(m->serve_sync, 0, P3D_SERVE_SYNC_ALL * sizeof(unsigned));
+  if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
+  __atomic_store_n(&m->errw[1], 0, __ATOMIC_SEQ_CST);
+  return fail(P3D_ERR_HIP, serve_err_text(v));
+}
+
 extern "C" int p3d_serve_check(p3d_model* m) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
-  if (!m->serve_err) return P3D_OK;
-  int v = 0;
-  hipError_t e = hipMemcpy(&v, m->serve_err, sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
-  if (v) {
-    // reported once: the word and the sync words are cleared, so later launches are judged
-    // on their own (every launch re-zeroes the sync words before it starts anyway)
-    if ((e = hipMemset(m->serve_sync, 0, (2 * P3D_SERVE_SYNC_WORDS + 64) * sizeof(unsigned))) != hipSuccess)
-      return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
-    m->serve_banks_clean = true;
-    return fail(P3D_ERR_HIP, v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
-                                    : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident)");
-  }
-  return P3D_OK;
+  const int v = __atomic_load_n(&m->errw[1], __ATOMIC_SEQ_CST);
+  return v ? serve_report(m, v) : P3D_OK;
 }
 
 extern "C" int p3d_sync_check(p3d_model* m) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
-  int v = 0;
-  hipError_t e = hipMemcpy(&v, m->xerr, sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_sync_check: ") + hipGetErrorString(e));
-  if (v) {
-    if ((e = hipMemset(m->xerr, 0, sizeof(int))) != hipSuccess)
-      return fail(P3D_ERR_HIP, std::string("p3d_sync_check: ") + hipGetErrorString(e));
+  if (__atomic_load_n(&m->errw[0], __ATOMIC_SEQ_CST)) {
+    __atomic_store_n(&m->errw[0], 0, __ATOMIC_SEQ_CST);
     return fail(P3D_ERR_HIP, "p3d_sync_check: a BN-train exchange timed out (row-tile workgroups not all resident)");
+  }
+  return P3D_OK;
+}
+
+// The error words as the kernels left them, read from pinned host memory: no device round trip,
+// no synchronisation (a caller checks after a synchronisation it makes anyway: a loss read, an
+// output copy).  flags: bit 0 an exchange timed out, bit 1 a serve spin ran out, bit 2 a serve
+// placement the launch was not sized for.  With clear != 0 the reported words are reset (a
+// reported serve error also clears the serve sync words: that part synchronises).
+extern "C" int p3d_error_flags(p3d_model* m, int32_t* flags, int32_t clear) {
+  if (!m || !flags) return fail(P3D_ERR_ARG, "p3d_error_flags: null argument");
+  const int x = __atomic_load_n(&m->errw[0], __ATOMIC_SEQ_CST), v = __atomic_load_n(&m->errw[1], __ATOMIC_SEQ_CST);
+  *flags = (x ? 1 : 0) | (v == 1 ? 2 : 0) | (v == 2 ? 4 : 0);
+  if (clear) {
+    if (x) __atomic_store_n(&m->errw[0], 0, __ATOMIC_SEQ_CST);
+    if (v) {
+      (void)serve_report(m, v);
+      g_err.clear();
+    }
   }
   return P3D_OK;
 }
@@ -2600,9 +2660,12 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   bool dz_pk = false;         // dy is row-major; every later dz is packed
   int dsel = 0;
   const float* dres_next = nullptr;  // block-output gradient to add when differentiating an A-layer
-  // weight gradients batched into one launch after the loop, unless Adam is fused into them or
-  // per-layer gradient-ready events (bucketed DP all-reduce) need them layer by layer
-  const bool multi = m->wgrad_multi && m->gev.empty() && nl <= P3D_WG_MULTI;
+  // weight gradients batched into one launch after the loop -- or, with gradient-ready buckets
+  // (data-parallel all-reduce overlapping the backward), one launch per bucket as soon as its
+  // layers' dZ and BN-parameter gradients exist, followed by the bucket's event
+  const bool multi = m->wgrad_multi && nl <= P3D_WG_MULTI;
+  const bool bucketed = !m->gev.empty() && !c.max_norm && multi && m->bucket_lo.size() == m->gev.size();
+  size_t kb = 0;                     // next bucket
   WgradMulti mw{};
   if (m->fuse_adam) {
     mw.adam = 1; mw.af = *m->fuse_adam; mw.w = m->flat[0]; mw.m = m->flat[2]; mw.v = m->flat[3]; mw.gflat = grads;
@@ -2610,10 +2673,11 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   // fused single-GPU step: Adam's alpha formed once by the first backward launch, so the last
   // launch (which reads no step state) advances it -- no k_step_advance launch; optionally the
   // tiles of layer l + 1 ride the dgrad launch of layer l (k_dgrad_wg, P3D_WGRAD_ATTACH=1)
-  const bool fused_tail = multi && m->fuse_adam && m->train_split;
+  const bool fused_tail = multi && m->fuse_adam && m->train_split && !bucketed;
   const bool attach = fused_tail && m->wgrad_attach;
   if (fused_tail) mw.alpha_dev = m->alpha_dev;
   m->step_advanced = false;
+  m->alpha_ready = false;
   // a layer's weight gradient (+ fused Adam): into the batched launch, or launched now
   // fused single-GPU step, side form: once dgrad(l) has read W(l) and formed layer l - 1's
   // dgamma / dbeta, nothing later in the backward reads what dW + Adam(l) reads or writes (the
@@ -2643,6 +2707,19 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     go(ps, k_wgrad_multi, dim3(one.begin[1]), dim3(256), m->side, one);
     LAUNCH_CHECK("k_wgrad_multi (side)");
     side_used = true;
+    return P3D_OK;
+  };
+  auto flush_bucket = [&](int l) -> int {   // bucket kb ends at layer l: its tiles, then its event
+    if (!bucketed || kb >= m->bucket_lo.size() || l != m->bucket_lo[kb]) return P3D_OK;
+    if (mw.n > 0) {
+      ProfScope ps(m, "wgrad_bucket");
+      go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+      LAUNCH_CHECK("k_wgrad_multi (bucket)");
+      mw.n = 0;
+      mw.begin[0] = 0;
+    }
+    HIP_TRY(hipEventRecord(m->gev[kb], st));
+    ++kb;
     return P3D_OK;
   };
   auto emit = [&](const WgradArgs& wa) -> int {
@@ -2677,6 +2754,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       }
     } else {
       int rc = emit(wa);
+      if (!rc) rc = flush_bucket(l);
       if (rc) return rc;
     }
     if (l == 0) {
@@ -2684,7 +2762,6 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         int rc = emit(wa);
         if (rc) return rc;
       }
-      if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[0], st));
       break;
     }
     const Layer& pv = m->layers[l - 1];
@@ -2719,13 +2796,16 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     if (pv.bn) { a.dgamma = grads + pv.gamma; a.dbeta = grads + pv.beta; }
     if (m->train_split) {
       if (pv.bn) a.bnpart = m->bnpart;
-      // (not while gradient-ready events feed a concurrent all-reduce: its kernels hold CUs
-      // the exchange's siblings need resident together)
-      const bool xchg = pv.bn && use_xchg(m, a.K, a.M) && m->gev.empty();
+      // (also beside a concurrent bucket all-reduce: its kernels share CUs with the siblings,
+      // which delays a sibling's start but never blocks it -- the spins are bounded regardless)
+      const bool xchg = pv.bn && use_xchg(m, a.K, a.M);
       if (xchg) { a.xchg = 1; a.xs = xchg_site(m, nl + l - 1); }   // dz, dgamma, dbeta here
       const dim3 grid((a.K + 15) / 16, (a.M + 15) / 16);
       const bool carry = attach && mw.n > 0 && dz_pk;   // layer l + 1's dW + Adam tiles ride along
       if (fused_tail && is_out) { a.alpha_out = m->alpha_dev; a.af = *m->fuse_adam; }
+      if (m->alpha_af && is_out) {   // data-parallel step: alpha for p3d_adam_apply after the all-reduce
+        a.alpha_out = m->alpha_dev; a.af = *m->alpha_af; m->alpha_ready = true;
+      }
       {
         ProfScope ps(m, is_out ? "dgrad_out" : carry ? "dgrad_wgrad" : "dgrad_hidden");
         if (carry) {
@@ -2768,8 +2848,6 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       int rc = side ? emit_side(wa, l) : emit(wa);
       if (rc) return rc;
     }
-    // layer l's W and b (wgrad above) and its gamma/beta (bn_bwd of iteration l + 1) are final
-    if (!m->gev.empty() && !c.max_norm) HIP_TRY(hipEventRecord(m->gev[l], st));
     dz_cur = m->dz[l - 1];
     dz_pk = true;
   }
@@ -2779,6 +2857,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
     LAUNCH_CHECK("k_wgrad_multi");
   }
+  if (!m->gev.empty() && !bucketed && !c.max_norm)   // (per-layer k_wgrad form: every bucket at the end)
+    for (hipEvent_t e : m->gev) HIP_TRY(hipEventRecord(e, st));
   if (side_used) {   // join: the caller's stream (and a graph being captured on it) waits for the side
     HIP_TRY(hipEventRecord(m->sev[nl], m->side));
     HIP_TRY(hipStreamWaitEvent(st, m->sev[nl], 0));
@@ -2796,15 +2876,27 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   return P3D_OK;
 }
 
-extern "C" int p3d_grad_events(p3d_model* m, int32_t enable) {
-  if (!m) return fail(P3D_ERR_ARG, "p3d_grad_events: null model");
+extern "C" int p3d_grad_buckets(p3d_model* m, int32_t n, const int32_t* lowest) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_grad_buckets: null model");
+  const int nl = (int)m->layers.size();
+  if (n < 0 || n > nl || (n > 0 && !lowest)) return fail(P3D_ERR_ARG, "p3d_grad_buckets: bad bucket count");
+  for (int k = 0; k < n; ++k)   // contiguous, backward order, the last one ending at layer 0
+    if (lowest[k] < 0 || lowest[k] >= nl || (k > 0 && lowest[k] >= lowest[k - 1]) || (k == n - 1 && lowest[k] != 0))
+      return fail(P3D_ERR_ARG, "p3d_grad_buckets: lowest layers must decrease and end at layer 0");
   for (hipEvent_t e : m->gev) HIP_TRY(hipEventDestroy(e));
   m->gev.clear();
-  if (enable) {
-    m->gev.resize(m->layers.size(), nullptr);
-    for (hipEvent_t& e : m->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
+  m->bucket_lo.assign(lowest, lowest + n);
+  m->gev.resize((size_t)n, nullptr);
+  for (hipEvent_t& e : m->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return P3D_OK;
+}
+
+extern "C" int p3d_grad_events(p3d_model* m, int32_t enable) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_grad_events: null model");
+  std::vector<int32_t> lo;
+  if (enable)
+    for (int l = (int)m->layers.size() - 1; l >= 0; --l) lo.push_back(l);   // one bucket per layer
+  return p3d_grad_buckets(m, (int32_t)lo.size(), lo.data());
 }
 
 // flat range of layer l's trainables (TF creation order: W, b[, gamma, beta]), padding included
@@ -2816,11 +2908,11 @@ extern "C" int p3d_layer_grad_range(const p3d_model* m, int32_t layer, int64_t* 
   return P3D_OK;
 }
 
-extern "C" int p3d_stream_wait_grad(p3d_model* m, int32_t layer, void* stream) {
+extern "C" int p3d_stream_wait_grad(p3d_model* m, int32_t bucket, void* stream) {
   if (!m) return fail(P3D_ERR_ARG, "p3d_stream_wait_grad: null model");
-  if (m->gev.empty()) return fail(P3D_ERR_STATE, "p3d_stream_wait_grad: p3d_grad_events not enabled");
-  if (layer < 0 || layer >= (int32_t)m->gev.size()) return fail(P3D_ERR_ARG, "p3d_stream_wait_grad: bad layer");
-  HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, m->gev[layer], 0));
+  if (m->gev.empty()) return fail(P3D_ERR_STATE, "p3d_stream_wait_grad: no gradient buckets (p3d_grad_buckets)");
+  if (bucket < 0 || bucket >= (int32_t)m->gev.size()) return fail(P3D_ERR_ARG, "p3d_stream_wait_grad: bad bucket");
+  HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, m->gev[bucket], 0));
   return P3D_OK;
 }
 
@@ -2843,13 +2935,45 @@ extern "C" int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, i
   return rc;
 }
 
+// The data-parallel step's first half: p3d_train_fwd_bwd, with the step's Adam alpha (lr =
+// lr0 * decay_rate^(global_step / decay_steps), bias corrections from the device step state)
+// formed by the backward's first launch, so that p3d_adam_apply -- after the caller's gradient
+// all-reduce -- is one launch that also advances the step state.
+extern "C" int p3d_train_fwd_bwd_lr(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
+                                    float keep_prob, uint64_t seed, int64_t row_offset, float lr0,
+                                    float decay_steps, float decay_rate, float* loss_dev, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd_lr: null model");
+  if (!(decay_steps > 0.f)) return fail(P3D_ERR_ARG, "p3d_train_fwd_bwd_lr: decay_steps must be > 0");
+  AdamFuse af{};
+  af.st = m->dstate; af.lr_host = -1.0f; af.lr0 = lr0; af.decay_steps = decay_steps; af.decay_rate = decay_rate;
+  af.b1 = 0.9f; af.b2 = 0.999f; af.eps = 1e-8f;
+  m->dp_af = af;
+  m->alpha_af = &m->dp_af;
+  const int rc = p3d_train_fwd_bwd(m, x, t, B, y, keep_prob, seed, row_offset, loss_dev, stream);
+  m->alpha_af = nullptr;
+  return rc;
+}
+
+static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st);
+
+// The data-parallel step's second half (after the all-reduce of the flat gradient): TF1 Adam +
+// re-pack of every weight with the alpha the backward formed, the step state advanced in the
+// same launch.  Falls back to p3d_adam_step_decay's two launches when the backward formed no
+// alpha (the whole-batch BN kernels, P3D_TRAIN_SPLIT=0).
+extern "C" int p3d_adam_apply(p3d_model* m, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_adam_apply: null model");
+  if (m->dp_af.decay_steps <= 0.f) return fail(P3D_ERR_STATE, "p3d_adam_apply: no p3d_train_fwd_bwd_lr before it");
+  if (!m->alpha_ready)
+    return adam_launch(m, -1.0f, m->dp_af.lr0, m->dp_af.decay_steps, m->dp_af.decay_rate, (hipStream_t)stream);
+  m->alpha_ready = false;
+  return adam_launch(m, -2.0f, m->dp_af.lr0, m->dp_af.decay_steps, m->dp_af.decay_rate, (hipStream_t)stream);
+}
+
 // One whole single-GPU TF1 training step (session.run([updates, loss, ...]),
 // linear_model.py:225-237): forward + fused MSE + backward with the Adam update applied
 // inside the weight-gradient kernels (no separate optimizer pass, no gradient round trip
 // through HBM), then the step state advances.  --max_norm models (the clip's gradient needs
 // every G first) take the unfused sequence.  lr = lr0 * decay_rate^(global_step/decay_steps).
-static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, float rate, hipStream_t st);
-
 extern "C" int p3d_train_step(p3d_model* m, const float* x, const float* t, int64_t B, float* y,
                               float keep_prob, uint64_t seed, float lr0, float decay_steps, float decay_rate,
                               float* loss_dev, void* stream) {
@@ -2883,13 +3007,17 @@ static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, floa
   a.lr_host = lr_host; a.lr0 = lr0; a.decay_steps = steps; a.decay_rate = rate;
   a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
   a.wblocks = m->at.tile_begin[m->at.nw];
+  const bool pre = lr_host == -2.0f;   // alpha formed by the backward (p3d_adam_apply): advance in-launch
+  if (pre) { a.alpha_dev = m->alpha_dev; a.advance = m->dstate; }
   {
     ProfScope ps(m, "adam_pack");
     go(ps, k_adam_pack, dim3(m->adam_blocks), dim3(256), st, a, m->at);
   }
   LAUNCH_CHECK("k_adam_pack");
-  k_step_advance<<<1, 1, 0, st>>>(m->dstate, a.b1, a.b2);
-  LAUNCH_CHECK("k_step_advance");
+  if (!pre) {
+    k_step_advance<<<1, 1, 0, st>>>(m->dstate, a.b1, a.b2);
+    LAUNCH_CHECK("k_step_advance");
+  }
   if (m->cfg.max_norm) {
     k_dot_partial<<<dim3(DOT_CHUNKS, m->wtab.n), 256, 0, st>>>(m->flat[0], m->flat[0], m->wtab, m->scratch);
     LAUNCH_CHECK("k_dot_partial");

@@ -59,6 +59,9 @@
 // of group g
 #define P3D_SERVE_FLAG0 256
 #define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 64)   // flags of up to 64 groups (k_serve6 S <= 8)
+// the model's serve sync allocation: k_serve6 banks 0 / 1, the k_serve5 bank, then k_serve6's
+// device epoch word (bank = epoch & 1) on a line of its own
+#define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 64)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
@@ -106,11 +109,14 @@ struct ServeArgs {
   int bn, residual; float eps;
   float* act;          // [8][3][64 * L] packed activations per XCD group
   float* part;         // [groups][2][L/16][4 * NDT * 256] output partials per XCD group (step parity)
-  unsigned* sync;      // P3D_SERVE_SYNC_WORDS, zeroed before every launch
-  int* err;            // set to 1 when a bounded spin ran out
+  unsigned* sync;      // k_serve5: its P3D_SERVE_SYNC_WORDS, zeroed before every launch; k_serve6: bank 0
+                       // of two consecutive banks (the launch picks one by *epoch)
+  int* err;            // host-visible (pinned) error word: 1 = a bounded spin ran out, 2 = a placement
+                       // the launch was not sized for
+  unsigned* epoch;     // k_serve6: launches so far (device-side, advanced by the launch itself)
+  int census_extra;    // test hook: the census waits for this many workgroups beyond the grid
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)
-  unsigned* sync_next; // k_serve6: the other sync-word bank, zeroed by this launch for the next
   const float* ecg;    // k_serve6: epilogue constants per layer and 16-column tile (k_serve_prep)
   ServeLayer ly[P3D_SERVE_MAXL];
 };
@@ -130,42 +136,45 @@ __device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_o
 // sh[1] = rank, sh[8 + x] = workgroups on XCD x, sh[2] = 1 if the wait timed out or an XCD
 // holds more than maxn workgroups (the flag barriers poll one lane per member).  In two
 // halves, so a kernel can do independent work between its arrival and the wait.
-__device__ __forceinline__ void p3d_serve_census_arrive(const ServeArgs& p, int* sh) {
+__device__ __forceinline__ void p3d_serve_census_arrive(unsigned* sync, int* sh) {
   if (threadIdx.x == 0) {
     unsigned xr;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
     const int xcc = (int)(xr & 7u);
     sh[0] = xcc;
-    sh[1] = (int)__hip_atomic_fetch_add(p.sync + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[1] = (int)__hip_atomic_fetch_add(sync + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
-__device__ __forceinline__ void p3d_serve_census_wait(const ServeArgs& p, int* sh, int maxn) {
+__device__ __forceinline__ void p3d_serve_census_wait(const ServeArgs& p, unsigned* sync, int* sh, int maxn) {
   if (threadIdx.x == 0) {
     int bad = 0, spin = 0;
     unsigned c[8];
+    const unsigned expect = gridDim.x + (unsigned)p.census_extra;
     while (true) {
       unsigned tot = 0;
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
-        c[x] = __hip_atomic_load(p.sync + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c[x] = __hip_atomic_load(sync + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tot += c[x];
       }
-      if (tot >= gridDim.x) break;
+      if (tot >= expect) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
     }
 #pragma unroll
-    for (int x = 0; x < 8; ++x) sh[8 + x] = (int)c[x];
-    if ((int)c[sh[0]] > maxn) bad = 1;
-    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int x = 0; x < 8; ++x) {
+      sh[8 + x] = (int)c[x];
+      if ((int)c[x] > maxn) bad = 1;   // judged on every XCD's count: all workgroups decide alike
+    }
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     sh[2] = bad;
   }
   __syncthreads();
 }
 __device__ __forceinline__ void p3d_serve_census(const ServeArgs& p, int* sh, int maxn) {
-  p3d_serve_census_arrive(p, sh);
-  p3d_serve_census_wait(p, sh, maxn);
+  p3d_serve_census_arrive(p.sync, sh);
+  p3d_serve_census_wait(p, p.sync, sh, maxn);
 }
 
 // ---- register ring -------------------------------------------------------------------
@@ -517,7 +526,7 @@ __global__ __launch_bounds__(512) void k_serve(ServeArgs p) {
           if (__all(v >= nsync)) break;
           if (++spin > P3D_SERVE_SPIN) {
             broken = true;
-            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
         }
@@ -724,7 +733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (__all(v >= nsync)) break;
         if (++spin > P3D_SERVE_SPIN) {
           broken = true;
-          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }

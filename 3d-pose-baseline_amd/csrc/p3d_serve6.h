@@ -11,8 +11,11 @@
 // each CU contracting <= 7 of a layer's 64 column tiles per phase -- 28 16x16 tiles of K = 1024
 // on the critical path and 4 phases, instead of 32 tiles and 8 phases.
 //
-// One launch per call: the sync words alternate between two banks (each launch zeroes the
-// other), the epilogue constants are formed in the prologue.
+// One launch per call: the sync words alternate between two banks picked on the device (the
+// launch reads an epoch word, uses bank epoch & 1, zeroes the other for the next launch, and one
+// workgroup advances the epoch once every workgroup has read it: the census guarantees that),
+// so a launch needs no memset in front and captured graphs replay correctly.  The epilogue
+// constants come from a table k_serve_prep forms per parameter version.
 //
 // What differs from k_serve5 (everything else -- census by hardware XCD id, flag hand-offs in
 // the XCD's L2, sc1 reads of other CUs' data, 4-wave K-split contraction with a register ring,
@@ -46,15 +49,13 @@
 #define P3D_S6_STAMP(row, k) do { } while (0)
 #endif
 
-// The serve launch's prologue kernel (in place of a memset of the sync words, so no extra
-// launch): zero the sync words and form the epilogue constants of every layer 0..2N and
-// column -- bias, inv = gamma / sqrt(var + eps), shift = beta - mean * inv, the arithmetic of
-// every other path -- laid out per 16-column tile as k_serve6 keeps them in LDS, so its
-// workgroups copy them with one round of loads instead of forming them (five dependent
-// operand loads per element) at the start of every launch.
+// The epilogue-constant table of the serve launches, formed when the parameters changed (and
+// inside every captured graph): bias, inv = gamma / sqrt(var + eps), shift = beta - mean * inv
+// -- the arithmetic of every other path -- of every layer 0..2N and column, laid out per
+// 16-column tile as k_serve6 keeps them in LDS, so its workgroups copy them with one round of
+// loads instead of forming them (five dependent operand loads per element) in every launch.
 __global__ __launch_bounds__(256) void k_serve_prep(ServeArgs p, float* ecg) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < P3D_SERVE_SYNC_WORDS) p.sync[i] = 0u;
   const int L = p.L, nl = 2 * p.nblk + 1;
   if (i >= nl * L) return;
   const int l = i / L, col = i % L, t = col >> 4, j = col & 15;
@@ -121,11 +122,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
 
   // ---- census: XCD id, rank within the XCD, wait for every workgroup ---------------------
-  // The sync words come in two banks used by alternate launches: this launch zeroes the
-  // other bank for the next one (stream order: the launch that used it has completed), so a
-  // launch needs no memset in front of it
+  // The sync words come in two banks used by alternate launches, picked by the device epoch
+  // word: this launch zeroes the other bank for the next one (stream order: the launch that
+  // used it has completed), so a launch needs no memset in front of it
+  if (tid == 0) {
+    sh[3] = (int)(__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u);
+    sh[4] = 0;                               // some wave of this workgroup is broken (group_sync)
+  }
+  __syncthreads();
+  const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
+  unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
   {
-    unsigned* other = p.sync_next;
+    unsigned* other = p.sync + (bank ^ 1) * P3D_SERVE_SYNC_WORDS;
     for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
   }
   // The census in two halves: after its arrival (XCD id, rank) a workgroup guesses its place
@@ -133,7 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // first input-layer operands and epilogue constants; the wait for every workgroup's arrival
   // then hides their latency.  The guess is used only if the final counts confirm it (every
   // workgroup sees the same counts, so all decide alike); otherwise the loads are re-issued.
-  p3d_serve_census_arrive(p, sh);
+  p3d_serve_census_arrive(sync, sh);
   const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
   constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
   // place of this workgroup for XCD counts cnt(x): member r of group gid (gi-th of ng groups
@@ -195,18 +203,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     place([&](int) { return nxg; }, xcc, rx, g_r, g_n, g_gid, g_gi, g_ng);
     prefetch(g_gi, (T * g_r) / g_n, (T * (g_r + 1)) / g_n);
   }
-  p3d_serve_census_wait(p, sh, (S < 1 || S > 8) ? -1 : 64 * S);
-  if (!sh[2]) {
+  p3d_serve_census_wait(p, sync, sh, (S < 1 || S > 8) ? -1 : 64 * S);
+  if (sh[2]) {
+    // the census failed (not every workgroup resident within the bounded wait): no row of this
+    // launch is computed; each workgroup fills a stripe of the output with NaN, so a caller who
+    // skips p3d_serve_check / p3d_error_flags still never reads a stale or unwritten row as a
+    // result (the error word is set)
+    const float qnan = __builtin_nanf("");
+    for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < p.M * p.ND; e += (int64_t)gridDim.x * 256) p.y[e] = qnan;
+  } else {
+  // every workgroup has read the epoch (before arriving): one of them advances it for the next
+  // launch -- rank 0 of the lowest-numbered XCD that holds workgroups (all see the same counts)
+  if (tid == 0 && sh[1] == 0) {
+    int lead = 0;
+    while (lead < 7 && sh[8 + lead] == 0) ++lead;
+    if (sh[0] == lead) __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   bool guess_held = guessable;
 #pragma unroll
   for (int x = 0; x < 8; ++x) guess_held = guess_held && __builtin_amdgcn_readfirstlane(sh[8 + x]) == nxg;
   int r, n, gid, gi, ng;
   place([&](int x) { return __builtin_amdgcn_readfirstlane(sh[8 + x]); }, xcc, rx, r, n, gid, gi, ng);
   if (gi < 0) {                              // a placement the host did not size this form for:
-    if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     gi = p.nb;                               // the whole group reports instead of computing
   }
-  unsigned* flags = p.sync + P3D_SERVE_FLAG0 + 64 * gid;   // (p.sync: this launch's bank)
+  unsigned* flags = sync + P3D_SERVE_FLAG0 + 64 * gid;   // (this launch's bank)
   const int64_t slab = (int64_t)ROWS * L;
   float* act = p.act + (int64_t)gid * 3 * slab;
   float* part = p.part + (int64_t)gid * 2 * T * PT;
@@ -283,11 +305,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // Group barrier (as k_serve5): drain, publish this member's phase, then each wave waits for
   // the members that produced its K slice (tiles [gb, gb + gcount)) -- or all members (full)
+  // A member whose wait ran out is `broken`: it publishes its phases with the poison bit, every
+  // member that reads a poisoned flag becomes broken too, and broken members store NaN instead
+  // of their output elements -- rows of a unit whose hand-offs failed never carry wrong values.
   auto group_sync = [&](bool full) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (broken) sh[4] = 1;
     __syncthreads();
+    broken = broken || sh[4] != 0;           // workgroup-wide from here (monotonic)
     ++nsync;
-    if (tid == 0) __hip_atomic_store(flags + r, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tid == 0)
+      __hip_atomic_store(flags + r, nsync | (broken ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int m0 = full ? 0 : p3d_tile_owner(gb, n, T);
     const int cnt = full ? n : p3d_tile_owner(gb + gcount - 1, n, T) - m0 + 1;
     if (!broken) {
@@ -295,10 +323,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       while (true) {
         const unsigned v = lane < cnt ? __hip_atomic_load(flags + m0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : nsync;
-        if (__all(v >= nsync)) break;
+        if (__all((v & 0x7fffffffu) >= nsync)) {
+          if (__any(v & 0x80000000u)) broken = true;
+          break;
+        }
         if (++spin > P3D_SERVE_SPIN) {
           broken = true;
-          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -362,11 +393,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       rsum[w * 64 * RE + el] = ss;
     }
   };
+  const float qnan = __builtin_nanf("");
   auto red_store = [&](int64_t prow0) {      // after a __syncthreads
     if (tid < ecnt) {
       f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 * RE + tid];
+      if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
       p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prow0);
     }
   };
@@ -382,6 +415,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int t = tb + 1; t < te; ++t) ss += p3d_ld_sc1(rs, (t * E4 + e4) * 16);
         sum += ss;
       }
+      if (broken) sum = f32x4{qnan, qnan, qnan, qnan};
       p3d_serve_store_out<NDT>(p, lo, sum, e4, prow0);
     }
   };

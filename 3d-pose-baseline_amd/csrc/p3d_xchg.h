@@ -13,8 +13,8 @@
 // partials inside the GEMM launch and each finishes its own tile.  The partials travel as
 // data-tagged granules (the R2 form of cdna_hip_programming.md Guideline 16: the data IS the
 // flag, no flag word, no fence, no drain before a signal):
-//   1. at kernel start lane 0 of wave 0 reads the site's epoch word (agent-scope load); the
-//      launch's tag is epoch + 1;
+//   1. at kernel start lane 0 of wave 0 reads its COLUMN TILE's epoch word (agent-scope load);
+//      the launch's tag is epoch + 1;
 //   2. after the GEMM, wave 0 stores its 16 columns' pairs as {a, tag, b, tag} 16-B write-through
 //      (sc1) stores into this site's slot array, one 256-B run per workgroup;
 //   3. wave 0 re-reads the R siblings' 16-B entries of its column with sc1 loads (L1 bypassed)
@@ -22,12 +22,15 @@
 //      them in row-tile order -- the association of the split form's second kernel, so both
 //      forms give the same bits (the helpers below are shared and compiled without FMA
 //      contraction);
-//   4. the row-tile-0 workgroup, once it has read every sibling's entry, adds 1 to the epoch
-//      word (agent atomic, no return).  Every sibling read the epoch before publishing, and
-//      row tile 0 adds only after it has seen all of them, so the epoch changes only after
-//      every sibling of this launch holds its tag: each launch's tag is unique without a
-//      memset in front (graph replays included), stale entries of earlier launches never match.
-// Each site (layer and direction) has its own epoch word and slot array.  The siblings of a
+//   4. the row-tile-0 workgroup of the column tile, once it has read every sibling's entry, adds
+//      1 to the tile's epoch word (agent atomic, no return).  Every sibling read that word before
+//      publishing, and row tile 0 adds only after it has seen all of them, so the word changes
+//      only after every sibling of this launch holds its tag: each launch's tag is unique
+//      without a memset in front (graph replays included), stale entries of earlier launches
+//      never match.  The word is the column tile's own (one 128-B line per tile): a shared word
+//      per site would move once per column tile, and a workgroup dispatched after another
+//      column tile had finished its swap would read a tag its siblings do not hold.
+// Each site (layer and direction) has its own epoch words and slot array.  The siblings of a
 // column tile have equal blockIdx % 8, i.e. one XCD under the observed round-robin placement
 // (speed only, never correctness).  Every sibling must be resident at once: the host uses this
 // form only when the grid fits on the device's CUs at one workgroup each.  Every spin is
@@ -70,15 +73,22 @@ __device__ __forceinline__ float p3d_bn_dz(float inv, float fm, float g, float s
 // ---- the exchange ------------------------------------------------------------------------
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+#define P3D_XCHG_EPOCH_STRIDE 32   // words between two column tiles' epoch words (one 128-B line each)
+
 struct XchgSite {
-  unsigned* epoch;   // one word (own 128-B line)
+  unsigned* epoch;   // per column tile one word, P3D_XCHG_EPOCH_STRIDE words apart
   float* slots;      // [P3D_XCHG_MAXR row tiles][N columns] 16-B entries {a, tag, b, tag}
-  int* err;
+  int* err;          // host-visible error word (pinned): 1 = a spin ran out
+  int delay;         // test hook (env P3D_XCHG_TEST_DELAY): odd column tiles' last row tile sleeps
+                     // ~delay x 3.4 us before reading its tag (a late-dispatched sibling)
 };
 
-// This launch's tag (wave-uniform; read at kernel start so its latency hides under the GEMM).
-__device__ __forceinline__ unsigned p3d_xchg_tag(const XchgSite& x) {
-  return __hip_atomic_load(x.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+// This launch's tag for column tile ct (wave-uniform; read at kernel start so its latency
+// hides under the GEMM).
+__device__ __forceinline__ unsigned p3d_xchg_tag(const XchgSite& x, int ct, int rt, int R) {
+  if (x.delay && (ct & 1) && rt == R - 1)
+    for (int i = 0; i < x.delay; ++i) __builtin_amdgcn_s_sleep(127);
+  return __hip_atomic_load(x.epoch + ct * P3D_XCHG_EPOCH_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 }
 
 // Wave 0, all 64 lanes: lanes with `mine` publish their column's pair (write-through).
@@ -107,15 +117,15 @@ __device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, in
       }
     if (__all(ok)) break;
     if (spin > P3D_XCHG_SPIN) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
 }
 
-// Row tile 0, after its swap: the next launch of this site gets a new tag.
-__device__ __forceinline__ void p3d_xchg_done(const XchgSite& x, int rt) {
+// Row tile 0 of column tile ct, after its swap: the tile's next launch gets a new tag.
+__device__ __forceinline__ void p3d_xchg_done(const XchgSite& x, int ct, int rt) {
   if (rt == 0 && (threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_add(x.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(x.epoch + ct * P3D_XCHG_EPOCH_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -80,8 +80,8 @@ def plan_buckets(ranges, min_elems):
 def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
     """Bucketed DP gradient average that overlaps the backward.
 
-    For each bucket (backward order), ``comm_stream`` waits for its layer's
-    gradient-ready event (``wait_ready(layer, stream_handle)``, p3d_stream_wait_grad),
+    For each bucket k (backward order), ``comm_stream`` waits for its gradient-ready event
+    (``wait_ready(k, stream_handle)``, p3d_stream_wait_grad),
     then an async all-reduce(AVG) of that slice is issued from it (RCCL); the current
     stream finally waits for all of them.  Every byte of ``t`` is reduced exactly once, so
     the result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).  Under gloo (tests:
@@ -94,8 +94,8 @@ def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
     if dist.get_backend() != "nccl":
         world = dist.get_world_size()
         with torch.cuda.stream(comm_stream):
-            for lo, hi, layer in buckets:
-                wait_ready(layer, comm_stream.cuda_stream)
+            for k, (lo, hi, _) in enumerate(buckets):
+                wait_ready(k, comm_stream.cuda_stream)
                 h = t[lo:hi].to("cpu")          # synchronous on comm_stream, after the event
                 dist.all_reduce(h, op=dist.ReduceOp.SUM)
                 h.div_(world)
@@ -104,8 +104,8 @@ def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
         return t
     works = []
     with torch.cuda.stream(comm_stream):
-        for lo, hi, layer in buckets:
-            wait_ready(layer, comm_stream.cuda_stream)
+        for k, (lo, hi, _) in enumerate(buckets):
+            wait_ready(k, comm_stream.cuda_stream)
             works.append(dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG, async_op=True))
     for w in works:
         w.wait()

@@ -127,6 +127,8 @@ class Saver:
         import tf_bundle
         path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
         self.model.sync_moving_stats()   # data parallel: one set of moving statistics
+        self.model.torch.cuda.synchronize(self.model.device)
+        self.model.check_errors()        # never save the result of a failed in-launch exchange
         if self.model.rank != 0:
             self._barrier()
             return path
@@ -164,8 +166,7 @@ class Saver:
         import checkpoint_io
         import tf_bundle
         if os.path.isfile(save_path + ".index"):
-            state = tf_bundle.read_bundle(save_path)
-            checkpoint_io.check_state(self.model, state)
+            state = checkpoint_io.check_state(self.model, tf_bundle.read_bundle(save_path))
             self.model.set_state(state)
             return
         p = save_path if save_path.endswith(".npz") else save_path + ".npz"
@@ -389,6 +390,11 @@ class LinearModel(object):
             check(lib().p3d_set_step(self._h, int(st["global_step"]), float(st["beta1_power"]),
                                      float(st["beta2_power"])), "p3d_set_step")
             self._step_host = int(st["global_step"])
+        if "learning_rate" in st:
+            # the reference decays from its restored learning_rate variable (src/linear_model.py:86-90):
+            # a reload with another --learning_rate continues with the checkpoint's
+            self.lr0 = float(np.asarray(st["learning_rate"], np.float32))
+            self._host_steps.clear()        # captured step graphs hold the old lr0
 
     def sync_moving_stats(self):
         """Data parallel: average the BN moving statistics over the replicas (each replica's
@@ -448,29 +454,36 @@ class LinearModel(object):
         B = x.shape[0]
         if out is None:
             out = self.torch.empty((B, self.output_size), dtype=self.torch.float32, device=self.device)
+        elif not (out.is_cuda and out.get_device() == self.device.index and out.dtype is torch.float32
+                  and out.is_contiguous() and tuple(out.shape) == (B, self.output_size)):
+            raise ValueError("serve_device: out must be a contiguous float32 [%d, %d] tensor on %s"
+                             % (B, self.output_size, self.device))
+        # (p3d_serve refuses to launch after an earlier launch failed until serve_check reported it)
         check(lib().p3d_serve(self._h, ptr(x), B, ptr(out), self.stream()), "p3d_serve")
         return out
 
     def serve_launcher(self, x, out):
         """A zero-argument callable that launches p3d_serve on the fixed device buffers x
-        [B, input_size] and out [B, output_size] on the current stream -- the serve_device
-        call with its argument checks and conversions done once, for serving loops over static
-        buffers.  The buffers must outlive the callable."""
+        [B, input_size] and out [B, output_size] on the stream current at each call -- the
+        serve_device call with its argument checks and conversions done once, for serving loops
+        over static buffers.  The buffers must outlive the callable."""
         import ctypes
         torch = self.torch
+        dev = self.device.index
         if not (isinstance(x, torch.Tensor) and x.dtype is torch.float32 and x.dim() == 2 and x.is_cuda and
-                x.is_contiguous() and x.shape[1] == self.input_size):
-            raise ValueError("serve_launcher: x must be a contiguous float32 [B, %d] device tensor" % self.input_size)
+                x.get_device() == dev and x.is_contiguous() and x.shape[1] == self.input_size):
+            raise ValueError("serve_launcher: x must be a contiguous float32 [B, %d] tensor on %s"
+                             % (self.input_size, self.device))
         B = x.shape[0]
         if not (isinstance(out, torch.Tensor) and out.dtype is torch.float32 and out.is_contiguous() and
-                tuple(out.shape) == (B, self.output_size) and out.is_cuda):
-            raise ValueError("serve_launcher: out must be a contiguous float32 [%d, %d] device tensor"
-                             % (B, self.output_size))
-        fn, args = lib().p3d_serve, (self._h, ctypes.c_void_p(x.data_ptr()), B,
-                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self.stream()))
+                tuple(out.shape) == (B, self.output_size) and out.is_cuda and out.get_device() == dev):
+            raise ValueError("serve_launcher: out must be a contiguous float32 [%d, %d] tensor on %s"
+                             % (B, self.output_size, self.device))
+        fn, h, px, po = lib().p3d_serve, self._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr())
+        stream_handle = _p3d.stream_handle
 
         def launch():
-            rc = fn(*args)
+            rc = fn(h, px, B, po, ctypes.c_void_p(stream_handle()))
             if rc:
                 check(rc, "p3d_serve")
         return launch
@@ -480,8 +493,27 @@ class LinearModel(object):
         check(lib().p3d_serve_check(self._h), "p3d_serve")
 
     def sync_check(self):
-        """Raise if a BN-train layer's in-launch exchange timed out (device read)."""
+        """Raise if a BN-train layer's in-launch exchange timed out (synchronises)."""
         check(lib().p3d_sync_check(self._h), "p3d_train")
+
+    def check_errors(self):
+        """Raise P3DError if a kernel that has completed reported a failed in-launch
+        synchronisation (BN-train exchange, serve census / hand-off).  No device round trip:
+        the error words live in pinned host memory the kernels write (p3d_error_flags), so the
+        callers check after a synchronisation they make anyway (loss read, output copy,
+        checkpoint save).  Reported once."""
+        import ctypes
+        f = ctypes.c_int32(0)
+        check(lib().p3d_error_flags(self._h, ctypes.byref(f), 0), "p3d_error_flags")
+        if f.value:
+            check(lib().p3d_error_flags(self._h, ctypes.byref(f), 1), "p3d_error_flags")
+            what = []
+            if f.value & 1:
+                what.append("a BN-train exchange timed out (row-tile workgroups not all resident): the step's "
+                            "batch statistics / gradients are invalid")
+            if f.value & 6:
+                what.append("a p3d_serve launch failed to synchronise its workgroups: its rows hold NaN")
+            raise _p3d.P3DError("; ".join(what))
 
     def loss_device(self, y, t, dy=None):
         B = y.shape[0]
@@ -513,14 +545,17 @@ class LinearModel(object):
                                        self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
                   "p3d_train_step")
         else:
-            # forward + fused MSE + backward, all-reduce of the flat gradient (in buckets that
-            # overlap the backward under RCCL), TF1 Adam
+            # forward + fused MSE + backward (the step's Adam alpha formed by its first launch;
+            # the weight gradients of each all-reduce bucket as one launch followed by the
+            # bucket's event), the all-reduce of the flat gradient (buckets overlapping the rest
+            # of the backward under RCCL), then TF1 Adam + re-pack + step advance in one launch
             if getattr(self, "_buckets", False) is False:   # first DP step: the default plan,
                 self.dp_buckets()                            # events on before the backward
-            check(lib().p3d_train_fwd_bwd(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
-                                          self.rank * B, ptr(loss_t), self.stream()), "p3d_train_fwd_bwd")
+            check(lib().p3d_train_fwd_bwd_lr(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
+                                             self.rank * B, self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
+                  "p3d_train_fwd_bwd_lr")
             self._allreduce_grads()
-            check(lib().p3d_adam_step_decay(self._h, self.lr0, 100000.0, 0.96, self.stream()), "p3d_adam_step")
+            check(lib().p3d_adam_apply(self._h, self.stream()), "p3d_adam_apply")
         self._step_host += 1
         return loss_t, y
 
@@ -540,16 +575,17 @@ class LinearModel(object):
 
     def dp_buckets(self, bucket_mb=None, gloo=False):
         """Enable (bucket_mb > 0) or disable (0) the bucketed gradient all-reduce that
-        overlaps the backward (env P3D_DP_BUCKET_MB, default 4 MB; RCCL by default, gloo --
-        host-staged, for tests of several ranks on one GPU -- when gloo=True).  Must be
-        called before a backward is issued.  Returns the bucket plan [(begin, end, layer)]."""
+        overlaps the backward (env P3D_DP_BUCKET_MB, default 8 MB: at cfg2 two buckets, {output,
+        hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two weight-gradient launches;
+        RCCL by default, gloo -- host-staged, for tests of several ranks on one GPU -- when
+        gloo=True).  Must be called before a backward is issued.  Returns the bucket plan
+        [(begin, end, lowest layer)] in backward order."""
         import ctypes
         import torch.distributed as dist
         if bucket_mb is None:
-            bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "4"))
+            bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "8"))
         on = (bucket_mb > 0 and self.data_parallel and dist.is_initialized()
               and (dist.get_backend() == "nccl" or gloo))
-        check(lib().p3d_grad_events(self._h, 1 if on else 0), "p3d_grad_events")
         self._buckets = None
         if on:
             ranges = []
@@ -558,16 +594,77 @@ class LinearModel(object):
                 check(lib().p3d_layer_grad_range(self._h, l, ctypes.byref(b), ctypes.byref(e)), "p3d_layer_grad_range")
                 ranges.append((b.value, e.value))
             self._buckets = dist_utils.plan_buckets(ranges, int(bucket_mb * (1 << 20)) // 4)
+            lo = (ctypes.c_int32 * len(self._buckets))(*[b[2] for b in self._buckets])
+            check(lib().p3d_grad_buckets(self._h, len(self._buckets), lo), "p3d_grad_buckets")
             self._comm = self.torch.cuda.Stream(device=self.device)
+        else:
+            check(lib().p3d_grad_buckets(self._h, 0, None), "p3d_grad_buckets")
         return self._buckets
 
     def _allreduce_grads(self):
         if getattr(self, "_buckets", None):
-            def wait(layer, handle):
-                check(lib().p3d_stream_wait_grad(self._h, layer, handle), "p3d_stream_wait_grad")
+            def wait(k, handle):
+                check(lib().p3d_stream_wait_grad(self._h, k, handle), "p3d_stream_wait_grad")
             dist_utils.allreduce_mean_buckets_(self.flat["grads"], self._buckets, wait, self._comm)
         else:
             dist_utils.allreduce_mean_(self.flat["grads"])
+
+    def train_step_graph(self, x, t, keep_prob, out=None, loss_out=None):
+        """Capture ONE training step on the fixed device buffers x [B, 32] / t [B, 48] into HIP
+        graph(s); returns a zero-argument callable that runs the next step (each call one
+        session.run of the train op, src/linear_model.py:225-237; the dropout counter, lr decay
+        and Adam state come from the device step state, so every replay is the next step).
+          * single GPU, or data parallel over RCCL: one graph of the whole step -- forward, backward,
+            the bucketed all-reduce (captured on the comm stream, forked from and joined to the
+            step by its bucket events) and the optimizer;
+          * data parallel over gloo (host-staged all-reduce, not capturable): a graph of forward
+            + backward, the host all-reduce of the flat gradient, a graph of the optimizer.
+        Bit-identical to the same steps through train_step_device (tests/test_gpu_dist.py).
+        Nothing runs at capture time; the model's step counter advances per call."""
+        import torch.distributed as dist
+        torch = self.torch
+        x = self._as_dev(x, self.input_size, "enc_in")
+        t = self._as_dev(t, self.output_size, "dec_out")
+        B = x.shape[0]
+        if out is None:
+            out = torch.empty((B, self.output_size), dtype=torch.float32, device=self.device)
+        loss_t = self._loss_dev if loss_out is None else loss_out
+        cur = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(cur)
+        gloo = self.data_parallel and dist.get_backend() != "nccl"
+        if not gloo:
+            if self.data_parallel and getattr(self, "_buckets", False) is False:
+                self.dp_buckets()              # events and comm stream exist before the capture
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                self.train_step_device(x, t, keep_prob, out=out, loss_out=loss_out)
+            self._step_host -= 1               # the capture issued no step
+            cur.wait_stream(side)
+
+            def step():
+                g.replay()
+                self._step_host += 1
+            step.graphs = (g,)
+            return step
+        if getattr(self, "_buckets", False) is not None:
+            self.dp_buckets(0)                 # one host all-reduce after the backward graph
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, stream=side, capture_error_mode="thread_local"):
+            check(lib().p3d_train_fwd_bwd_lr(self._h, ptr(x), ptr(t), B, ptr(out), float(keep_prob), self.seed,
+                                             self.rank * B, self.lr0, 100000.0, 0.96, ptr(loss_t),
+                                             _p3d.stream_handle()), "p3d_train_fwd_bwd_lr")
+        with torch.cuda.graph(g2, stream=side, capture_error_mode="thread_local"):
+            check(lib().p3d_adam_apply(self._h, _p3d.stream_handle()), "p3d_adam_apply")
+        cur.wait_stream(side)
+
+        def step():
+            g1.replay()
+            dist_utils.allreduce_mean_(self.flat["grads"])
+            g2.replay()
+            self._step_host += 1
+        step.graphs = (g1, g2)
+        return step
 
     # ------------------------------------------------------------------ reference API
     def step(self, session, encoder_inputs, decoder_outputs, dropout_keep_prob, isTraining=True):
@@ -587,6 +684,7 @@ class LinearModel(object):
                 loss, y = self.train_step_device(encoder_inputs, decoder_outputs, dropout_keep_prob)
                 out = y.cpu().numpy()
                 lv = float(loss.item())
+                self.check_errors()
                 return lv, Summary("loss/loss", lv), Summary("learning_rate/learning_rate", lr), out
             x = self._as_dev(encoder_inputs, self.input_size, "enc_in")
             t = self._as_dev(decoder_outputs, self.output_size, "dec_out")
@@ -594,6 +692,7 @@ class LinearModel(object):
             loss = self.loss_device(y, t)
             out = y.cpu().numpy()
             lv = float(loss.item())
+            self.check_errors()
             return lv, Summary("loss/loss", lv), out
 
     # ---- step() from host arrays: the session.run path with one H2D, one D2H, one sync ------
@@ -688,6 +787,7 @@ class LinearModel(object):
             st["hy"].copy_(st["dy"], non_blocking=True)
             st["hl"].copy_(loss, non_blocking=True)
         stream.synchronize()
+        self.check_errors()
         lv = float(st["hl_np"][0])
         out = st["hy_np"].copy()
         if training:

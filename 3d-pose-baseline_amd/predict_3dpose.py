@@ -119,7 +119,7 @@ class Session:
         raise NotImplementedError("Session.run: unsupported fetch %r" % (fetches,))
 
 
-def create_model(session, actions, batch_size, flags=None):
+def create_model(session, actions, batch_size, flags=None, load_exact=False):
     """src/predict_3dpose.py:131-186: build the model, init fresh or restore --load."""
     flags = flags or FLAGS
     tdir = train_dir_for(flags)
@@ -132,14 +132,20 @@ def create_model(session, actions, batch_size, flags=None):
     if flags.load <= 0:
         print("Creating model with fresh parameters.")
         return model
+    # src/predict_3dpose.py:163-181, including its behaviour: --load N checks that
+    # checkpoint-N.index exists, then restores the checkpoint the directory's `checkpoint` file
+    # names as the latest (ckpt.model_checkpoint_path, :180) -- not necessarily N.  Pass
+    # load_exact=True (a keyword of this build) to restore checkpoint-N itself.
     import tf_bundle
-    if tf_bundle.read_checkpoint_state(tdir) is None and not os.path.isdir(tdir):
-        raise ValueError("Checkpoint directory {0} does not seem to exist".format(tdir))
+    latest = tf_bundle.read_checkpoint_state(tdir)
+    if latest is None:
+        raise ValueError("Checkpoint directory {0} does not seem to hold a checkpoint".format(tdir))
     ck = os.path.join(tdir, "checkpoint-{0}".format(flags.load))
     if not (os.path.isfile(ck + ".index") or os.path.isfile(ck + ".npz")):
         raise ValueError("Asked to load checkpoint {0}, but it does not seem to exist".format(flags.load))
-    print("Loading model {0}".format(ck))
-    model.saver.restore(session, ck)
+    path = ck if load_exact else latest
+    print("Loading model {0}".format(os.path.basename(ck)))
+    model.saver.restore(session, path)
     return model
 
 
@@ -238,6 +244,7 @@ def evaluate_batches(sess, model, data_mean_3d, data_std_3d, dim_to_use_3d, dim_
         run_eval_rows(model, acc, X, Y, model.batch_size)
         js = acc.joint_sum.cpu().numpy()
         loss = float(acc.loss_sum(model.batch_size).item())
+        model.check_errors()
     step_time = (time.time() - start) / max(nbatches, 1)
     n = max(acc.frames, 1)
     joint_err = js / n
@@ -276,6 +283,7 @@ def evaluate_action_wise(model, test_set_2d, test_set_3d, data_mean_3d, data_std
             table[ai, J + 1] = acc.loss_sum(model.batch_size)[0]
         dist_utils.allreduce_sum_(table)
         t = table.cpu().numpy()
+        model.check_errors()
     errs = {}
     for ai, action in enumerate(actions):
         n = max(t[ai, J], 1.0)
@@ -378,6 +386,7 @@ def train(flags=None):
                                                 loss_out=losses[i:i + 1])
                         if (i + 1) % log_every_n_batches == 0:
                             step_loss = float(losses[i].item())
+                            model.check_errors()     # (after the sync the loss read made)
                             model.train_writer.add_summary(linear_model.Summary("loss/loss", step_loss), current_step)
                             model.train_writer.add_summary(
                                 linear_model.Summary("learning_rate/learning_rate", lr), current_step)
@@ -387,6 +396,7 @@ def train(flags=None):
                                 epoch, i + 1, nbatches, 1000 * step_time / log_every_n_batches))
                         current_step += 1
                     loss = float(losses[:nbatches].double().sum().item())
+                    model.check_errors()
             else:
                 for i in range(nbatches):
                     step_loss, loss_summary, lr_summary, _ = model.step(sess, enc[i], dec[i], flags.dropout,

@@ -90,6 +90,22 @@ def setup_dist():
     return rank, world, dev
 
 
+def init_world1_group():
+    """A 1-rank RCCL process group (127.0.0.1 rendezvous) so the data-parallel train step --
+    bucketed all-reduce included -- can be timed on one GPU beside the fused single-GPU step."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return False
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    return True
+
+
 def barrier_sync(world):
     import torch
     import torch.distributed as dist
@@ -489,17 +505,23 @@ def bench_infer(args, rank, world):
     return value, dt, roof, single
 
 
-def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
-    """cfg3: K training steps (fwd + MSE + bwd + [all-reduce] + fused TF1 Adam/re-pack) of
-    64 poses per GPU.  Single GPU: G steps captured in one HIP graph (all step state is
-    device-resident: dropout counter, lr decay, beta powers).  Data parallel: eager steps
-    with RCCL all-reduce(AVG) of the 17.17 MB flat gradient per step, in buckets of
-    ``bucket_mb`` that overlap the backward (0: one all-reduce after it)."""
+def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None, dp=None):
+    """cfg3: K training steps (fwd + MSE + bwd + [all-reduce] + TF1 Adam/re-pack) of 64 poses
+    per GPU, captured in HIP graphs (all step state is device-resident: dropout counter, lr
+    decay, beta powers).  Single GPU: the fused step (Adam inside the weight-gradient launch),
+    G steps per graph.  Data parallel over RCCL: G whole DP steps per graph -- the bucketed
+    all-reduce(AVG) of the 17.17 MB flat gradient (buckets of ``bucket_mb``, one weight-gradient
+    launch each, overlapping the rest of the backward; 0: one all-reduce after it) captured on
+    the comm stream; over gloo (rehearsal: several ranks on one GPU) per-step graphs around the
+    host-staged all-reduce (LinearModel.train_step_graph).  ``dp`` forces the data-parallel
+    form (e.g. on a 1-rank RCCL group: the DP step's compute beside the fused single-GPU step)."""
     import torch
+    import torch.distributed as dist
     steps = steps or args.steps
     warmup = warmup if warmup is not None else args.warmup
-    model, _ = make_model(data_parallel=world > 1)
-    if world > 1:
+    dp = (world > 1) if dp is None else dp
+    model, _ = make_model(data_parallel=dp)
+    if dp:
         model.dp_buckets(args.dp_bucket_mb if bucket_mb is None else bucket_mb)
     rng = np.random.default_rng(200 + rank)
     G = 16
@@ -513,19 +535,26 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         for i in range(k):
             model.train_step_device(X[i % G], T[i % G], args.keep, out=Y)
 
-    use_graph = world == 1 or args.train_graph
+    gloo = dp and dist.is_initialized() and dist.get_backend() != "nccl"
+    use_graph = not args.train_eager
     run(max(2, warmup // 4))
     torch.cuda.synchronize()
-    if use_graph:
+    mode = "eager"
+    if use_graph and gloo:
+        # host-staged all-reduce between a forward+backward graph and an optimizer graph per step
+        steps_g = [model.train_step_graph(X[i], T[i], args.keep, out=Y) for i in range(G)]
+        fn, per, mode = (lambda: [f() for f in steps_g]), G, "graph"
+    elif use_graph:
         s0 = torch.cuda.Stream()
         s0.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s0):
             run(G)
         torch.cuda.current_stream().wait_stream(s0)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             run(G)
-        fn, per = graph.replay, G
+        model._step_host -= G
+        fn, per, mode = graph.replay, G, "graph"
     else:
         fn, per = (lambda: run(G)), G
     for _ in range(max(1, warmup // per)):
@@ -548,7 +577,8 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
         achieved = byts / (avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _committed_traffic("k_adam_pack", {"mode": "train", "batch": BATCH}),
-                "kernel": "k_adam_pack", "bytes_per_launch": byts, "avg_us": round(avg_us, 3)}
+                "kernel": "k_adam_pack (TF1 Adam + Wf/Wd re-pack + step advance, after the all-reduce)",
+                "bytes_per_launch": byts, "avg_us": round(avg_us, 3)}
     else:
         # single GPU (p3d_train_step): Adam runs inside the weight-gradient kernels; per step
         # they read X and dZ, read+write W, m, v, write Wf, Wd (4 B each), and update the
@@ -580,8 +610,15 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "bytes_per_step": int(byts), "avg_us": round(avg_us, 3), "launches_timed": cnt}
     roof["event_pair_avg_us"] = {k: round(v[1], 3) for k, v in prof.items()}
+    # the whole step against HBM: SURVEY 8d's algorithmic bytes of one cfg3 step (parameters,
+    # gradients, both Adam slots read and written: 8 x 17.17 MB) over the measured step time
+    step_bytes = 8 * 4 * n_params
+    ms = 1000.0 * dt / steps
+    roof["step"] = {"bytes_per_step": step_bytes, "ms_per_step": round(ms, 5),
+                    "achieved": round(step_bytes / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     model.close()
-    return value, dt, roof, ("graph" if use_graph else "eager")
+    return value, dt, roof, mode
 
 
 def bench_eval(args, rank, world):
@@ -963,10 +1000,11 @@ def main():
                     help="pick the inference streams by observed hardware-queue concurrency")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--train-graph", action="store_true", help="graph-capture DP training steps too")
+    ap.add_argument("--train-eager", action="store_true", help="train steps without HIP graphs")
+    ap.add_argument("--no-dp1", action="store_true", help="skip the 1-rank data-parallel train form (infer mode)")
     ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
     ap.add_argument("--keep", type=float, default=0.5, help="dropout keep_prob of the train step")
-    ap.add_argument("--dp-bucket-mb", type=float, default=4.0,
+    ap.add_argument("--dp-bucket-mb", type=float, default=8.0,
                     help="data-parallel gradient all-reduce bucket (MB) overlapping the backward; 0 = one all-reduce")
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
@@ -1016,6 +1054,22 @@ def main():
                          "roofline": troof}
             except Exception as exc:  # report, never lose the headline line
                 train = {"error": repr(exc)[:300]}
+            if world == 1 and not args.no_dp1 and "error" not in train:
+                try:   # the data-parallel step's form on a 1-rank RCCL group (what each rank runs at N > 1)
+                    own = init_world1_group()
+                    dv, ddt, droof, dmode = bench_train(args, rank, world, steps=args.train_steps, warmup=64, dp=True)
+                    train["dp_form_1rank"] = {
+                        "workload": "the data-parallel step (fwd + bwd with %g MB gradient buckets, one weight-gradient "
+                                    "launch each, RCCL all-reduce(AVG) on a 1-rank group, TF1 Adam + re-pack + step "
+                                    "advance in one launch)" % args.dp_bucket_mb,
+                        "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
+                        "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
+                        "event_pair_avg_us": droof.get("event_pair_avg_us")}
+                    if own:
+                        import torch.distributed as dist
+                        dist.destroy_process_group()
+                except Exception as exc:
+                    train["dp_form_1rank"] = {"error": repr(exc)[:300]}
             if world > 1 and args.dp_bucket_mb > 0 and "error" not in train:
                 try:   # the same steps with one all-reduce after the backward (no overlap)
                     sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=0)

@@ -126,14 +126,28 @@ int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t tr
  * (other kernels merely delay it).  A launch whose workgroups could not all synchronise
  * stops within ~0.5 s and is reported by the next p3d_serve_check (P3D_ERR_HIP). */
 int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
-/* 0 if every p3d_serve launch so far completed its synchronisation (device read; syncs). */
+/* 0 if every p3d_serve launch so far completed its synchronisation (synchronises the device,
+ * then reads the kernels' pinned error word).  After a failure p3d_serve refuses new launches
+ * (P3D_ERR_HIP) until this call reports it once; the failed launch's rows hold NaN, never
+ * unwritten or stale values.  k_serve6 launches pick their sync-word bank on the device, so a
+ * captured p3d_serve replays correctly (its epilogue-constant table is re-formed in the graph). */
 int p3d_serve_check(p3d_model* m);
 
-/* 0 if every BN-train exchange so far completed (device read; syncs).  Training layers with
- * batch norm run as one launch each whose row-tile workgroups swap their column statistics
- * inside the launch; a spin that ran out (workgroups not co-resident, e.g.
- * another persistent kernel holding CUs) sets a word this reports once, as P3D_ERR_HIP. */
+/* 0 if every BN-train exchange so far completed (synchronises, then reads the pinned error word).
+ * Training layers with batch norm run as one launch each whose row-tile workgroups swap their
+ * column statistics inside the launch; a spin that ran out (workgroups not
+ * co-resident, e.g. another persistent kernel holding CUs) sets a word this reports once, as
+ * P3D_ERR_HIP. */
 int p3d_sync_check(p3d_model* m);
+
+/* The kernels' error words without any device round trip or synchronisation: they live in
+ * pinned, mapped host memory the kernels write directly, so a caller reads them after a
+ * synchronisation it makes anyway (a loss read, an output copy).  *flags: bit 0 a BN-train
+ * exchange timed out, bit 1 a p3d_serve spin ran out, bit 2 a p3d_serve placement the launch
+ * was not sized for.  clear != 0 resets what was reported (a serve error also re-zeroes the
+ * serve sync words, which synchronises).  Replaces no reference interface: TF raised op
+ * errors from session.run (src/linear_model.py:236,244). */
+int p3d_error_flags(p3d_model* m, int32_t* flags, int32_t clear);
 
 /* MSE loss of linear_model.py:129 and its gradient: loss = mean((y-t)^2) over
  * B*D, dy = (1/(B*D)) * 2*(y-t).  loss_dev: one device float (may be NULL),
@@ -153,17 +167,34 @@ int p3d_train_fwd_bwd(p3d_model* m, const float* x, const float* t, int64_t B, f
                       float keep_prob, uint64_t seed, int64_t row_offset, float* loss_dev,
                       void* stream);
 
-/* Gradient-ready events for a bucketed data-parallel all-reduce (the DP form of
- * opt.compute_gradients -> apply_gradients, linear_model.py:143-145).
- * p3d_grad_events(m, 1) makes every later p3d_backward / p3d_train_fwd_bwd record one event
- * per layer l (0 = input layer .. 2N+1 = output layer) on its stream as soon as the flat grads
- * range [begin, end) of p3d_layer_grad_range(m, l) is final -- the output layer's first, the
- * input layer's last, so the all-reduce of late layers overlaps the backward of earlier ones.
- * p3d_stream_wait_grad makes another stream wait for layer l's event of the last backward.
- * (--max_norm models: every event after the clip's gradient, i.e. at the end.) */
+/* Gradient-ready buckets for a data-parallel all-reduce that overlaps the backward (the DP
+ * form of opt.compute_gradients -> apply_gradients, linear_model.py:143-145).
+ * p3d_grad_buckets(m, n, lowest): bucket k covers the layers from the previous bucket's lowest
+ * minus one down to lowest[k] (layers 0 = input .. 2N+1 = output; buckets in backward order,
+ * lowest[] strictly decreasing, lowest[n-1] == 0; n == 0 turns the buckets off).  Every later
+ * p3d_backward / p3d_train_fwd_bwd[_lr] then runs the weight gradients of bucket k as ONE
+ * k_wgrad_multi launch as soon as its layers' dZ and BN-parameter gradients exist (right after
+ * the data-gradient launch of the layer above lowest[k]) and records bucket k's event, so the
+ * bucket's flat range (p3d_layer_grad_range of its layers, contiguous) is final at that event
+ * and its all-reduce overlaps the rest of the backward.  p3d_stream_wait_grad makes another
+ * stream wait for bucket k's event of the last backward.  p3d_grad_events(m, 1) = one bucket
+ * per layer.  (--max_norm models: every event after the clip's gradient, i.e. at the end.) */
+int p3d_grad_buckets(p3d_model* m, int32_t n, const int32_t* lowest);
 int p3d_grad_events(p3d_model* m, int32_t enable);
 int p3d_layer_grad_range(const p3d_model* m, int32_t layer, int64_t* begin, int64_t* end);
-int p3d_stream_wait_grad(p3d_model* m, int32_t layer, void* stream);
+int p3d_stream_wait_grad(p3d_model* m, int32_t bucket, void* stream);
+
+/* The data-parallel step (session.run of the train op with the gradient averaged over the
+ * replicas, linear_model.py:137-145 + SURVEY 8e) in two calls around the caller's all-reduce of
+ * the flat grads buffer: p3d_train_fwd_bwd_lr = p3d_train_fwd_bwd whose first backward launch
+ * also forms the step's Adam alpha (lr0 * decay_rate^(global_step / decay_steps), TF1 bias
+ * correction, from the device step state); p3d_adam_apply = TF1 ApplyAdam + weight re-pack with
+ * that alpha, the step state (global_step, beta powers) advanced in the same launch.  Both are
+ * graph-capturable (all step state on the device). */
+int p3d_train_fwd_bwd_lr(p3d_model* m, const float* x, const float* t, int64_t B, float* y, float keep_prob,
+                         uint64_t seed, int64_t row_offset, float lr0, float decay_steps, float decay_rate,
+                         float* loss_dev, void* stream);
+int p3d_adam_apply(p3d_model* m, void* stream);
 
 /* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
  * the TF1 Adam update, global_step += 1.  By default (env P3D_FUSE_ADAM=1 at p3d_create) the

@@ -215,12 +215,17 @@ def test_train_steps_track_oracle(split, xchg, monkeypatch):
     m.close()
 
 
-@pytest.mark.parametrize("L,B,keep", [(1024, 64, 0.5), (256, 17, 0.5), (256, 64, 1.0), (256, 200, 0.5)])
-def test_bn_exchange_bit_identical_to_split(L, B, keep, monkeypatch):
+@pytest.mark.parametrize("L,B,keep,delay", [(1024, 64, 0.5, 0), (256, 17, 0.5, 0), (256, 64, 1.0, 0),
+                                           (256, 200, 0.5, 0), (1024, 64, 0.5, 8), (256, 200, 0.5, 8)])
+def test_bn_exchange_bit_identical_to_split(L, B, keep, delay, monkeypatch):
     """BN-train layers as ONE launch (row-tile workgroups swap their column statistics in the
     launch, p3d_xchg.h) == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit, over 4
     fused train steps: outputs, loss, weights, Adam slots, moving statistics.  B = 200 (13 row
-    tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4."""
+    tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4.
+    delay > 0 (test hook P3D_XCHG_TEST_DELAY): the last row-tile workgroup of every odd column
+    tile sleeps ~27 us before it reads its tag, so other column tiles finish their swaps (and
+    advance their epochs) first -- with one epoch word per site that late sibling read a tag
+    its siblings did not hold (advisor r2); with the column tile's own word it must not matter."""
     import ctypes
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=2, residual=True, batch_norm=True)
@@ -228,6 +233,7 @@ def test_bn_exchange_bit_identical_to_split(L, B, keep, monkeypatch):
     ms = []
     for flag in ("1", "0"):
         monkeypatch.setenv("P3D_TRAIN_XCHG", flag)
+        monkeypatch.setenv("P3D_XCHG_TEST_DELAY", str(delay if flag == "1" else 0))
         m = linear_model.LinearModel(L, 2, True, True, False, B, 1e-3, "/tmp/p3d_test", seed=9, max_batch=max(B, 64))
         m.set_weights({**st.params, **st.moving})
         ms.append(m)
@@ -248,6 +254,7 @@ def test_bn_exchange_bit_identical_to_split(L, B, keep, monkeypatch):
         assert torch.equal(ys[0], ys[1]), step
         assert torch.equal(xm._loss_dev, sm._loss_dev), step
     xm.sync_check()
+    xm.check_errors()
     for k in ("params", "moving", "adam_m", "adam_v"):
         if xm.flat[k] is not None:
             assert torch.equal(xm.flat[k], sm.flat[k]), k

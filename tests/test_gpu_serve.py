@@ -281,3 +281,78 @@ def test_serve6_constants_follow_parameter_updates():
     ro, _ = ref_mlp.forward(st2, xd.cpu().numpy(), False, 1.0, 0, 0, 0)
     close(y2.cpu().numpy(), ro)
     m.close()
+
+
+def test_serve_census_failure_reports_and_fills_nan(monkeypatch):
+    """A launch whose census cannot complete (test hook P3D_SERVE_TEST_FAULT: the census waits
+    for one workgroup more than the grid) ends within its bounded spin, fills its rows with
+    NaN (never unwritten or stale rows), sets the pinned error word (read without a device
+    round trip, LinearModel.check_errors), and p3d_serve refuses further launches until the
+    error is collected; serve_check reports it once (P3D_ERR_HIP)."""
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    monkeypatch.setenv("P3D_SERVE_TEST_FAULT", "1")
+    st, m = make(cfg)
+    monkeypatch.delenv("P3D_SERVE_TEST_FAULT")
+    x = torch.randn((64 * 5 + 3, 32), device="cuda")
+    y = torch.zeros((x.shape[0], 48), device="cuda")
+    m.serve_device(x, out=y)
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(y).all()), "failed launch left non-NaN rows"
+    with pytest.raises(_p3d.P3DError, match="earlier launch failed"):
+        m.serve_device(x, out=y)                      # refused: nobody collected the error
+    with pytest.raises(_p3d.P3DError, match="synchronisation timed out"):
+        m.serve_check()
+    m.serve_check()                                   # reported once
+    # the pinned-word path (no device round trip): the next failure surfaces in check_errors
+    m.serve_device(x, out=y)
+    torch.cuda.synchronize()
+    with pytest.raises(_p3d.P3DError, match="p3d_serve launch failed"):
+        m.check_errors()
+    m.check_errors()                                  # cleared
+    m.close()
+    # a healthy model on the same device is unaffected
+    st2, m2 = make(cfg)
+    x2 = np.random.default_rng(9).standard_normal((64 * 3, 32)).astype(np.float32)
+    y2 = m2.serve_device(torch.from_numpy(x2).cuda()).cpu().numpy()
+    m2.serve_check()
+    ro, _ = ref_mlp.forward(st2, x2, False, 1.0, 0, 0, 0)
+    close(y2, ro)
+    m2.close()
+
+
+def test_serve_graph_replay_follows_inputs_and_parameters():
+    """p3d_serve captured in a HIP graph (advisor r2: the sync-word bank was picked on the host
+    and the epilogue constants formed at capture time): every replay alternates the banks on
+    the device and re-forms the constants, so replays with new inputs and new parameters equal
+    the eager batch-64 kernels."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    B = 64 * 20
+    x = torch.zeros((B, 32), device="cuda")
+    y = torch.zeros((B, 48), device="cuda")
+    m.serve_device(x, out=y)                          # warm-up (tables, buffers)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        m.serve_device(x, out=y)
+    rng = np.random.default_rng(21)
+    for rep in range(6):
+        x.copy_(torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)))
+        if rep == 3:      # new parameters between replays (as a training graph would change them)
+            st2 = ref_mlp.init_state(cfg, seed=31, bn_seed=32)
+            m.set_weights({**st2.params, **st2.moving})
+            st = st2
+        g.replay()
+        torch.cuda.synchronize()
+        ref = torch.cat([m.forward_device(x[i:i + 64]) for i in range(0, B, 64)])
+        torch.cuda.synchronize()
+        d = (y - ref).abs()
+        assert bool((d <= 5e-5 + 5e-5 * ref.abs()).all()), (rep, float(d.max()))
+    m.serve_check()
+    ro, _ = ref_mlp.forward(st, x.cpu().numpy(), False, 1.0, 0, 0, 0)
+    close(y.cpu().numpy(), ro)
+    del g
+    m.close()

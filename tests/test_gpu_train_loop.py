@@ -35,3 +35,40 @@ def test_device_loop_matches_step_loop():
     assert ga == gb and ga[0] > 0
     for k in wa:
         np.testing.assert_array_equal(wa[k], wb[k], err_msg=k)
+
+
+def test_create_model_load_restores_latest(tmp_path):
+    """create_model(--load N) after a real train() run (src/predict_3dpose.py:163-181): two
+    epochs write checkpoint-S1 and checkpoint-S2; --load S1 checks that checkpoint-S1.index
+    exists and then restores the checkpoint the directory's `checkpoint` file names as the
+    latest (S2) -- the reference's own behaviour (:180 restores ckpt.model_checkpoint_path);
+    load_exact=True (this build's keyword) restores S1 itself; a missing N raises ValueError."""
+    import checkpoint_io
+    import tf_bundle
+    tdir = str(tmp_path)
+    args = ["--synthetic", "--epochs", "2", "--linear_size", "256", "--num_layers", "1", "--residual",
+            "--batch_norm", "--dropout", "0.5", "--learning_rate", "1e-3", "--train_dir", tdir]
+    np.random.seed(7)
+    flags = predict_3dpose.build_parser().parse_args(args)
+    model = predict_3dpose.train(flags)
+    final = model.get_state()
+    model.close()
+    ck_dir = predict_3dpose.train_dir_for(flags)
+    latest = tf_bundle.read_checkpoint_state(ck_dir)
+    s2 = int(latest.rsplit("-", 1)[1])
+    s1 = s2 // 2
+    assert s1 > 0 and os.path.isfile(os.path.join(ck_dir, "checkpoint-%d.index" % s1))
+    assert int(final["global_step"]) == s2
+    first = tf_bundle.read_bundle(os.path.join(ck_dir, "checkpoint-%d" % s1))
+    lflags = predict_3dpose.build_parser().parse_args(args + ["--load", str(s1)])
+    for exact, want in ((False, final), (True, first)):
+        m = predict_3dpose.create_model(None, ["All"], lflags.batch_size, lflags, load_exact=exact)
+        got = m.get_state()
+        for k in checkpoint_io.global_order(m.param_table):
+            np.testing.assert_array_equal(np.asarray(got[k], np.float64), np.asarray(want[k], np.float64),
+                                          err_msg="%s (load_exact=%s)" % (k, exact))
+        assert m.get_step()[0] == (s1 if exact else s2)
+        m.close()
+    with pytest.raises(ValueError, match="does not seem to exist"):
+        bad = predict_3dpose.build_parser().parse_args(args + ["--load", str(s1 + 1)])
+        predict_3dpose.create_model(None, ["All"], bad.batch_size, bad)
