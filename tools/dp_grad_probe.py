@@ -40,12 +40,21 @@ def worker(rank, world, port, out, L, B, keep):
     ts = rng.standard_normal((2, B, 48))
     m.step(None, xs[0], ts[0], keep, isTraining=True)
     after0 = m.get_weights(include_moving=True)
+    am0, av0 = m.flat["adam_m"].cpu().numpy().copy(), m.flat["adam_v"].cpu().numpy().copy()
     x1 = torch.from_numpy(xs[1].astype(np.float32)).cuda()
     t1 = torch.from_numpy(ts[1].astype(np.float32)).cuda()
     loss, y = m.compute_gradients(x1, t1, keep, ctr=1)
     torch.cuda.synchronize()
     g = {n: m.grad(n).cpu().numpy().copy() for n in m.trainable_names()}
-    flat = {}
+    # and the real second DP step: averaged gradient (left in the grads buffer) and the update
+    m.set_weights({k: v for k, v in after0.items()})   # compute_gradients moved the moving stats
+    m.step(None, xs[1], ts[1], keep, isTraining=True)
+    torch.cuda.synchronize()
+    flat = {"am0": am0, "av0": av0, "gavg": m.flat["grads"].cpu().numpy().copy(),
+            "p1": m.flat["params"].cpu().numpy().copy(), "p0flat": None}
+    flat.pop("p0flat")
+    offs = {n: (o, k) for n, k, kind, o in [(a, b, c, d) for a, b, c, d in m.param_table] if kind == 0}
+    flat["w2off"] = np.int64(offs["linear_model/two_linear_0/w2_0"][0])
     for tag, d in (("init", init), ("after0", after0), ("grad", g)):
         for n, v in d.items():
             flat[tag + "/" + n] = v
@@ -87,7 +96,30 @@ def main(out_json, L=1024, B=64, keep=0.5):
         for n in gr:
             scale = float(np.abs(gr[n]).max()) or 1.0
             report["grad"].setdefault(n, {})["rank%d" % r] = float(np.abs(rs[r]["grad/" + n] - gr[n]).max()) / scale
+    # the second step's update of w2_0 on the GPU vs TF1 Adam (fp64) from the GPU's own state
+    # and averaged gradient, and vs the oracle's averaged gradient
+    off = int(r0["w2off"])
+    n2 = "linear_model/two_linear_0/w2_0"
+    sz = params[n2].size
+    p0 = r0["after0/" + n2].reshape(-1).astype(np.float64)
+    m0, v0 = r0["am0"][off:off + sz].astype(np.float64), r0["av0"][off:off + sz].astype(np.float64)
+    ggpu = r0["gavg"][off:off + sz].astype(np.float64)
+    p1 = r0["p1"][off:off + sz].astype(np.float64)
+    b1p, b2p = 0.9 ** 2, 0.999 ** 2
+    alpha = 1e-3 * np.sqrt(1 - b2p) / (1 - b1p)
+    def adam(g):
+        mm = m0 + (g - m0) * 0.1
+        vv = v0 + (g * g - v0) * 0.001
+        return p0 - mm * alpha / (np.sqrt(vv) + 1e-8)
+    gref = (rs[0]["grad/" + n2].reshape(-1) + rs[1]["grad/" + n2].reshape(-1)).astype(np.float64) / 2
+    e_gpu_adam = np.abs(adam(ggpu) - p1)
+    i = int(np.argmax(e_gpu_adam))
+    report["w2_0_step1"] = {"adam_from_gpu_grad_max": float(e_gpu_adam.max()), "at": i,
+                            "g_gpu": float(ggpu[i]), "g_avg_of_rank_grads": float(gref[i]),
+                            "m0": float(m0[i]), "v0": float(v0[i]), "p0": float(p0[i]), "p1": float(p1[i]),
+                            "grad_avg_vs_rank_grads_max": float(np.abs(ggpu - gref).max())}
     json.dump(report, open(out_json, "w"), indent=1)
+    print(json.dumps(report["w2_0_step1"]))
     print(json.dumps(report["out"]))
     print(json.dumps(sorted(((max(v.values()), k) for k, v in report["grad"].items()), reverse=True)[:6]))
 

@@ -1,6 +1,7 @@
 """Phase timestamps of the BN-train hidden forward kernel (dev tool).
 
-Needs the tracing build:  hipcc ... -DP3D_TRACE -o 3d-pose-baseline_amd/libp3d_trace.so
+Needs the tracing build (RS = 1: the default 256-workgroup exchange form):
+    hipcc ... -DP3D_TRACE -DP3D_TRACE_RS=1 -o 3d-pose-baseline_amd/libp3d_trace.so
     P3D_LIB=$PWD/3d-pose-baseline_amd/libp3d_trace.so python tools/trace_train.py [keep]
 Prints, per phase, the min/median/max over workgroups of the wall_clock64 (100 MHz) delta
 from the earliest workgroup start of the last traced launch.
@@ -29,9 +30,18 @@ lib = _p3d.lib()
 lib.p3d_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(4096 * 8, np.uint64)
 assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
-t = buf.reshape(4096, 8)[:64, :6].astype(np.int64)   # 64 workgroups of the RS=4 launch
+nwg = int(os.environ.get("P3D_TRACE_NWG", "256"))   # workgroups of the traced launch
+t = buf.reshape(4096, 8)[:nwg, :6].astype(np.int64)
 t0 = t[:, 0].min()
-names = ["start", "gemm(w0)", "reduced", "bn", "philox", "stored"]
+names = ["start", "gemm(w0)", "reduced", "bn+xchg", "philox", "stored"]
 for k, n in enumerate(names):
     d = (t[:, k] - t0) * 10.0 / 1000.0
     print("%-9s min %6.2f  med %6.2f  max %6.2f us" % (n, d.min(), np.median(d), d.max()))
+# per column tile: the latest sibling's GEMM end vs each sibling's exchange end (arrival skew)
+gx = nwg // 4
+g = (t[:, 2] - t0).reshape(4, gx) * 10.0 / 1000.0
+b = (t[:, 3] - t0).reshape(4, gx) * 10.0 / 1000.0
+print("sibling skew of 'reduced' (max-min over the 4 row tiles): med %.2f max %.2f us"
+      % (np.median(g.max(0) - g.min(0)), (g.max(0) - g.min(0)).max()))
+print("exchange done - latest sibling reduced: med %.2f max %.2f us"
+      % (np.median(b - g.max(0)), (b - g.max(0)).max()))
