@@ -86,26 +86,49 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
                                                 float* wf, float alpha, float omb1, float omb2, float eps) {
   const int tid = threadIdx.x;
   const bool vec = (N & 3) == 0;
+  if (vec) {
+    // all four rows' w / m / v (and g) requested before the first update, from clamped (always
+    // valid) addresses, stores after: a load inside the per-row range branch made every row a
+    // dependent memory round trip (with the previous row's stores in the same wait)
+    f32x4 ww[4], mm[4], vv[4], gg[4];
+    bool ok[4];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
-    const int k = k0 + r, n = n0 + c;
-    float wn[4] = {0.f, 0.f, 0.f, 0.f};
-    if (k < K) {
-      const int64_t base = off + (int64_t)k * N + n;
-      if (vec && n + 3 < N) {
-        f32x4 ww = *(f32x4*)(w + base), mm = *(f32x4*)(m + base), vv = *(f32x4*)(v + base);
-        f32x4 gg;
-        if (g) gg = *(const f32x4*)(g + base);
-        else gg = f32x4{tile[r][c], tile[r][c + 1], tile[r][c + 2], tile[r][c + 3]};
+    for (int it = 0; it < 4; ++it) {
+      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+      const int k = k0 + r, n = n0 + c;
+      ok[it] = k < K && n < N;
+      const int64_t base = ok[it] ? off + (int64_t)k * N + n : off;
+      ww[it] = *(const f32x4*)(w + base);
+      mm[it] = *(const f32x4*)(m + base);
+      vv[it] = *(const f32x4*)(v + base);
+      if (g) gg[it] = *(const f32x4*)(g + base);
+      else gg[it] = f32x4{tile[r][c], tile[r][c + 1], tile[r][c + 2], tile[r][c + 3]};
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+      const int64_t base = off + (int64_t)(k0 + r) * N + n0 + c;
+      float wn[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ok[it]) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float w1 = ww[e], m1 = mm[e], v1 = vv[e];
-          p3d_adam1(w1, m1, v1, gg[e], alpha, omb1, omb2, eps);
-          ww[e] = w1; mm[e] = m1; vv[e] = v1; wn[e] = w1;
+          float w1 = ww[it][e], m1 = mm[it][e], v1 = vv[it][e];
+          p3d_adam1(w1, m1, v1, gg[it][e], alpha, omb1, omb2, eps);
+          ww[it][e] = w1; mm[it][e] = m1; vv[it][e] = v1; wn[e] = w1;
         }
-        *(f32x4*)(w + base) = ww; *(f32x4*)(m + base) = mm; *(f32x4*)(v + base) = vv;
-      } else {
+        *(f32x4*)(w + base) = ww[it]; *(f32x4*)(m + base) = mm[it]; *(f32x4*)(v + base) = vv[it];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];   // each thread rewrites only what it read
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+      const int k = k0 + r, n = n0 + c;
+      float wn[4] = {0.f, 0.f, 0.f, 0.f};
+      if (k < K) {
+        const int64_t base = off + (int64_t)k * N + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (n + e < N) {
@@ -115,9 +138,9 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
             wn[e] = ww;
           }
       }
-    }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];   // each thread rewrites only what it read
+      for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];
+    }
   }
   __syncthreads();
   const int NP = (N + 15) & ~15;
@@ -166,14 +189,26 @@ struct FwdArgs {
   int64_t lddy;
   float* lossp;                   //   per-workgroup sum of (y - t)^2
   XchgSite xs;                    // bn == 4 (BN-train exchange form, p3d_xchg.h)
+  int remap_gy;                   // > 0: 1-D grid of gx * remap_gy blocks, tiles by p3d_sibling_remap
 };
+
+// Tile of block b in a 1-D grid of gx * gy blocks (gx % 8 == 0): the gy row-tile siblings of a
+// column tile are blocks xcd + 8 j for gy consecutive j -- one XCD under the observed round-robin
+// placement, dispatched together (the 2-D grid put them 64 blocks apart).  Speed only: the
+// exchange is correct for any placement.
+__device__ __forceinline__ void p3d_sibling_remap(int b, int gx, int gy, int& ct, int& rt) {
+  const int xcd = b & 7, j = b >> 3;
+  rt = j % gy;
+  ct = (j / gy) * 8 + xcd;
+  (void)gx;
+}
 
 // Phase timestamps for kernel development (build with -DP3D_TRACE; tools/trace_train.py).
 #ifdef P3D_TRACE
 #define P3D_STAMP(k)                                                                             \
   do {                                                                                           \
-    if ((threadIdx.x & 63) == 0 && (blockIdx.x + gridDim.x * blockIdx.y) < 4096)                 \
-      g_p3d_trace[(blockIdx.x + gridDim.x * blockIdx.y) * 8 + (k)] = wall_clock64();             \
+    if ((threadIdx.x & 63) == 0 && p3d_trace_idx < 4096)                                          \
+      g_p3d_trace[p3d_trace_idx * 8 + (k)] = wall_clock64();                                     \
   } while (0)
 extern "C" int p3d_debug_trace(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p3d_trace), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : 2;
@@ -189,11 +224,19 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int ct = blockIdx.x, n0 = ct * 16, m0 = blockIdx.y * 16 * RS;
+  int tbx = blockIdx.x, tby = blockIdx.y, tgx = gridDim.x, tgy = gridDim.y;
+  if (p.remap_gy > 0) {
+    tgx = (p.N + 15) >> 4;
+    tgy = p.remap_gy;
+    p3d_sibling_remap(blockIdx.x, tgx, tgy, tbx, tby);
+  }
+  const int ct = tbx, n0 = ct * 16, m0 = tby * 16 * RS;
   const int col = n0 + i;
   const bool cok = col < p.N;
   const int cc = cok ? col : p.N - 1;
   const int ngN = (p.N + 15) >> 4;
+  const int p3d_trace_idx = tbx + tgx * tby;
+  (void)p3d_trace_idx;
 #ifndef P3D_TRACE_RS
 #define P3D_TRACE_RS 4
 #endif
@@ -213,7 +256,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   uint64_t ctr = p.ctr;
   unsigned xtag = 0;
   if (w == 0) {
-    if (p.bn == 4) xtag = p3d_xchg_tag(p.xs, ct, blockIdx.y, gridDim.y);
+    if (p.bn == 4) xtag = p3d_xchg_tag(p.xs, ct, tby, tgy);
     if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
     b = p.bias[cc];
     if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
@@ -235,7 +278,12 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   p3d_core<RS, DEPTH, NACC, APK>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
   if (trace) P3D_STAMP(1);
   if (trace_last) P3D_STAMP(6);
-  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
+  __shared__ XchgPub xpub;                  // bn == 4: wave 0 posts its column pairs, wave 1 publishes
+  if (WK > 1 && p.bn == 4 && w == 1) p3d_xchg_pub_reset(&xpub);
+  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) {
+    if (WK > 1 && p.bn == 4 && w == 1) p3d_xchg_publish(p.xs, &xpub, p.N, tby, n0);
+    return;
+  }
   if (trace) P3D_STAMP(2);
   // ---- epilogue (wave 0): lane holds rows m0+16s+4q+r of column n0+i ---------------
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
@@ -266,16 +314,24 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
         if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mt; sq += d * d; }
     sq = p3d_colsum16(sq);
     if (p.bn == 4) {
-      const int R = (int)gridDim.y;
+      const int R = tgy;
       float st[P3D_XCHG_MAXR], qt[P3D_XCHG_MAXR];
-      p3d_xchg_put(p.xs, p.N, blockIdx.y, col, q == 0 && cok, sum, sq, xtag);
+      if (WK > 1) p3d_xchg_post(&xpub, q == 0, i, sum, sq, xtag);
+      else p3d_xchg_put(p.xs, p.N, tby, col, q == 0 && cok, sum, sq, xtag);
       // the dropout uniforms do not depend on the statistics: formed while the siblings arrive
       if (p.keep < 1.0f) {
 #pragma unroll
         for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu_x[s]);
       }
-      p3d_xchg_get(p.xs, p.N, R, cc, xtag, st, qt);
-      p3d_xchg_done(p.xs, ct, blockIdx.y);
+      p3d_xchg_get(p.xs, p.N, R, cc, xtag, st, qt, tby);
+      p3d_xchg_done(p.xs, ct, tby);
+#ifdef P3D_TRACE
+      if (trace && lane == 0 && p3d_trace_idx < 4096) {   // slot 7: the hardware XCD of this workgroup
+        unsigned xr;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+        g_p3d_trace[p3d_trace_idx * 8 + 7] = xr & 7u;
+      }
+#endif
       float S = 0.f;
 #pragma unroll
       for (int t = 0; t < P3D_XCHG_MAXR; ++t)
@@ -292,8 +348,8 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   if (p.bn == 3) {
     if (!cok) return;
     if (q == 0) {
-      p.bnpart[((int64_t)blockIdx.y * p.N + col) * 2] = sum;
-      p.bnpart[((int64_t)blockIdx.y * p.N + col) * 2 + 1] = sq;
+      p.bnpart[((int64_t)tby * p.N + col) * 2] = sum;
+      p.bnpart[((int64_t)tby * p.N + col) * 2 + 1] = sq;
     }
 #pragma unroll
     for (int s = 0; s < RS; ++s)
@@ -307,7 +363,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   float inv = 1.0f, shift = 0.0f;
   if (p.bn == 4) {
     p3d_bn_affine(xmean, xvar, p.eps, gam, bet, inv, shift);
-    if (blockIdx.y == 0 && q == 0 && cok) {
+    if (tby == 0 && q == 0 && cok) {
       p.mean_save[col] = xmean;
       p.var_save[col] = xvar;
       p.mmean[col] = p3d_bn_moving(mmu, xmean, p.decay);
@@ -372,7 +428,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
-    if (lane == 0) p.lossp[blockIdx.x + gridDim.x * blockIdx.y] = ls;
+    if (lane == 0) p.lossp[tbx + tgx * tby] = ls;
   }
   if (!cok) return;
 #pragma unroll
@@ -610,6 +666,7 @@ struct BwdArgs {
   const float* lossp; int nlossp; // fused MSE: workgroup 0 folds the forward's loss partials
   float* loss; float loss_scale;  //   (fixed order) into loss[0] = scale * sum
   XchgSite xs; int xchg;          // with bnpart: exchange form (p3d_xchg.h) -- dz, dgamma, dbeta here
+  int remap_gy;                   // > 0: 1-D grid of (K/16) * remap_gy blocks (p3d_sibling_remap)
   float* alpha_out; AdamFuse af;  // fused Adam: tile (0, 0) stores the step's alpha for later launches
 };
 
@@ -659,17 +716,27 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
   p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, m0, p.Wd, ngt, ct, gb, ge, acc);
-  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
+  __shared__ XchgPub xpub;                  // exchange form: wave 0 posts its column sums, wave 1 publishes
+  const bool pubw = WK > 1 && p.xchg && p.prev && p.bn && w == 1;
+  if (pubw) p3d_xchg_pub_reset(&xpub);
+  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) {
+    if (pubw) p3d_xchg_publish(p.xs, &xpub, p.K, by, n0);
+    return;
+  }
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
-  float g[RS][4];
+  // exchange form: the residual-gradient stores wait until after the swap (the sweeps' vmcnt
+  // waits would otherwise wait for them too)
+  const bool defer_draw = WK > 1 && p.xchg && p.prev && p.bn;
+  float g[RS][4], dv[RS][4];
 #pragma unroll
   for (int s = 0; s < RS; ++s)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + 16 * s + 4 * q + r;
       const float d = (p.wsq ? acc[0][s][r] / mx : acc[0][s][r]) + dr[s][r];
-      if (p.draw && cok && row < p.M) p.draw[p3d_pk(row, col, ngK)] = d;
+      if (p.draw && cok && row < p.M && !defer_draw) p.draw[p3d_pk(row, col, ngK)] = d;
       g[s][r] = d;
+      dv[s][r] = d;
     }
   if (!p.prev) return;
   // previous layer: y = dropout(relu(BN(z))) ; recompute a = BN(z) for the relu mask
@@ -709,9 +776,18 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
     if (p.xchg) {   // exchange form: the row-tile siblings swap {sum g, sum g xhat}
       const int R = gy;
       float at[P3D_XCHG_MAXR], bt[P3D_XCHG_MAXR];
-      p3d_xchg_put(p.xs, p.K, by, col, q == 0 && cok, sg, sgx, xtag);
-      p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt);
+      if (WK > 1) p3d_xchg_post(&xpub, q == 0, i, sg, sgx, xtag);
+      else p3d_xchg_put(p.xs, p.K, by, col, q == 0 && cok, sg, sgx, xtag);
+      p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt, by);
       p3d_xchg_done(p.xs, bx, by);
+      if (defer_draw && p.draw && cok)
+#pragma unroll
+        for (int s = 0; s < RS; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + 16 * s + 4 * q + r;
+            if (row < p.M) p.draw[p3d_pk(row, col, ngK)] = dv[s][r];
+          }
       sg = 0.f;
       sgx = 0.f;
 #pragma unroll
@@ -761,6 +837,12 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
 
 template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
 __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
+  if (p.remap_gy > 0) {
+    int bx, by;
+    p3d_sibling_remap(blockIdx.x, (p.K + 15) >> 4, p.remap_gy, bx, by);
+    p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, bx, by, p.remap_gy);
+    return;
+  }
   p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
@@ -842,28 +924,57 @@ struct WgradArgs {
 
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
 
-// Stage rows [mc, mc+64) x cols [c0, c0+64) of a packed or row-major [R, C] source.
-__device__ __forceinline__ void p3d_stage64(float* __restrict__ dst, const float* __restrict__ src, int pk, int64_t ld,
-                                            int R, int C, int mc, int c0) {
+// Stage rows [mc, mc+64) x cols [c0, c0+64) of a packed or row-major [R, C] source, in two
+// halves so that both operands' loads are in flight before the first LDS write: every load from
+// a clamped (always valid) address, out-of-range elements zeroed after it.  (A load behind a
+// per-element range branch made the compiler wait for each load on its own: 8 dependent memory
+// round trips per staged chunk.)
+struct Stage64 { float f[16]; unsigned ok; };
+__device__ __forceinline__ void p3d_stage64_load(Stage64& st, const float* __restrict__ src, int pk, int64_t ld,
+                                                 int R, int C, int mc, int c0) {
   const int tid = threadIdx.x;
+  st.ok = 0u;
   if (pk) {  // 16 packed 1 KB tiles (4 row tiles x 4 column groups); C is a multiple of 16
     const int ng = C >> 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int idx = tid + 256 * e, chunk = idx >> 6, ln = idx & 63;
       const int rt = chunk >> 2, gg = chunk & 3;
-      const int row = 16 * rt + (ln & 15), col = 16 * gg + 4 * (ln >> 4);
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (mc + row < R && c0 + 16 * gg < C)
-        v = ((const f32x4*)src)[((int64_t)((mc >> 4) + rt) * ng + (c0 >> 4) + gg) * 64 + ln];
-      *(f32x4*)&dst[row * WG_LDS_STRIDE + col] = v;
+      const int row = 16 * rt + (ln & 15);
+      const bool ok = mc + row < R && c0 + 16 * gg < C;
+      st.ok |= ok ? (1u << e) : 0u;
+      const int64_t off = ok ? ((int64_t)((mc >> 4) + rt) * ng + (c0 >> 4) + gg) * 64 + ln : 0;
+      const f32x4 v = ((const f32x4*)src)[off];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st.f[4 * e + j] = v[j];
     }
   } else {
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int m = e >> 6, c = e & 63;
-      float v = 0.f;
-      if (mc + m < R && c0 + c < C) v = src[(int64_t)(mc + m) * ld + c0 + c];
-      dst[m * WG_LDS_STRIDE + c] = v;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + 256 * k, m = e >> 6, c = e & 63;
+      const bool ok = mc + m < R && c0 + c < C;
+      st.ok |= ok ? (1u << k) : 0u;
+      st.f[k] = src[ok ? (int64_t)(mc + m) * ld + c0 + c : 0];
+    }
+  }
+}
+__device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const Stage64& st, int pk) {
+  const int tid = threadIdx.x;
+  if (pk) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e, chunk = idx >> 6, ln = idx & 63;
+      const int rt = chunk >> 2, gg = chunk & 3;
+      const int row = 16 * rt + (ln & 15), col = 16 * gg + 4 * (ln >> 4);
+      const bool ok = (st.ok >> e) & 1u;
+      *(f32x4*)&dst[row * WG_LDS_STRIDE + col] =
+          ok ? f32x4{st.f[4 * e], st.f[4 * e + 1], st.f[4 * e + 2], st.f[4 * e + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + 256 * k, m = e >> 6, c = e & 63;
+      dst[m * WG_LDS_STRIDE + c] = ((st.ok >> k) & 1u) ? st.f[k] : 0.f;
     }
   }
 }
@@ -881,9 +992,14 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
   __shared__ float dbp[4][64];
   const bool do_db = p.db && by == 0;
   float dbs = 0.f;   // wave w: rows 16w .. 16w+15 of column `lane` (summed in row order)
+  // the step's alpha, requested before the contraction (its latency hides there)
+  const float alpha_pre = (p.adam && p.alpha_dev) ? *p.alpha_dev : 0.f;
   for (int mc = 0; mc < p.M; mc += 64) {
-    p3d_stage64(xs, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
-    p3d_stage64(zs, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
+    Stage64 sx, sz;
+    p3d_stage64_load(sx, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
+    p3d_stage64_load(sz, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
+    p3d_stage64_store(xs, sx, p.xpk);
+    p3d_stage64_store(zs, sz, p.zpk);
     __syncthreads();
 #pragma unroll 4
     for (int t = 0; t < 16; ++t) {
@@ -904,7 +1020,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
   }
   float alpha = 0.f;
   if (p.adam)
-    alpha = p.alpha_dev ? *p.alpha_dev : p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
+    alpha = p.alpha_dev ? alpha_pre : p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
   if (do_db) {
     dbp[w][lane] = dbs;
     __syncthreads();
@@ -1315,6 +1431,7 @@ struct p3d_model {
                               // 128-B line each), then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
   int64_t xslots_off = 0;     // word offset of the slot arrays in xsync
   int xchg_delay = 0;         // test hook: late row-tile siblings (env P3D_XCHG_TEST_DELAY, p3d_xchg.h)
+  int xchg_remap = 1;         // exchange launches as 1-D grids with the siblings on one XCD (env P3D_XCHG_REMAP)
   // error words the kernels write and the host reads without a device round trip (pinned, mapped):
   // [0] a BN-train exchange / split-K hand-off timed out, [1] a p3d_serve launch failed (1: a spin
   // ran out, 2: an XCD group smaller than the launch was sized for)
@@ -1685,7 +1802,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     if ((e = hipDeviceGetAttribute(&m->num_cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return cleanup(e);
     m->xslots_off = (int64_t)2 * nl * (L / 16) * P3D_XCHG_EPOCH_STRIDE;
-    const int64_t nx = m->xslots_off + (int64_t)2 * nl * P3D_XCHG_MAXR * L * 4;
+    const int64_t nx = m->xslots_off + (int64_t)2 * 2 * nl * P3D_XCHG_MAXR * L * 4;   // sc1 + plain copies
     if ((e = hipMalloc(&m->xsync, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->xsync, 0, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     if ((e = hipHostMalloc((void**)&m->errw, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
@@ -1697,6 +1814,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     m->serve_err = dv + 1;
   }
   if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
+  if (const char* ev = getenv("P3D_XCHG_REMAP")) m->xchg_remap = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_TEST_FAULT")) m->serve_fault = atoi(ev);
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
@@ -1938,9 +2056,9 @@ static XchgSite xchg_site(const p3d_model* m, int slot) {
   XchgSite x;
   x.epoch = m->xsync + (int64_t)slot * (L / 16) * P3D_XCHG_EPOCH_STRIDE;
   x.slots = (float*)(m->xsync + m->xslots_off) + (int64_t)slot * P3D_XCHG_MAXR * L * 4;
+  x.near = x.slots + (int64_t)2 * nl * P3D_XCHG_MAXR * L * 4;
   x.err = m->xerr;
   x.delay = m->xchg_delay;
-  (void)nl;
   return x;
 }
 
@@ -1952,8 +2070,10 @@ static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream
     a.bn = 4; a.xs = xchg_site(m, a.site);
     static const char* tags[2] = {"fwd_in_train_x", "fwd_hidden_train_x"};
     ProfScope ps(m, tags[kind == 0 ? 0 : 1]);
-    if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, grid, dim3(512), st, a);
-    else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, grid, dim3(512), st, a);
+    dim3 g = grid;
+    if (m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
+    if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, g, dim3(512), st, a);
+    else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, g, dim3(512), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
   }
@@ -2813,9 +2933,13 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, dim3((unsigned)(gx * gy + mw.begin[mw.n])), dim3(512), st, a, mw,
              gx, gy);
         } else if (dz_pk) {
-          go(ps, k_dgrad<1, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
+          dim3 g = grid;
+          if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
+          go(ps, k_dgrad<1, 8, 8, 2, true, 1>, g, dim3(512), st, a);
         } else {
-          go(ps, k_dgrad<1, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
+          dim3 g = grid;
+          if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
+          go(ps, k_dgrad<1, 8, 8, 2, false, 2>, g, dim3(512), st, a);
         }
       }
       LAUNCH_CHECK("k_dgrad");

@@ -15,13 +15,20 @@
 // flag, no flag word, no fence, no drain before a signal):
 //   1. at kernel start lane 0 of wave 0 reads its COLUMN TILE's epoch word (agent-scope load);
 //      the launch's tag is epoch + 1;
-//   2. after the GEMM, wave 0 stores its 16 columns' pairs as {a, tag, b, tag} 16-B write-through
-//      (sc1) stores into this site's slot array, one 256-B run per workgroup;
-//   3. wave 0 re-reads the R siblings' 16-B entries of its column with sc1 loads (L1 bypassed)
-//      until every tag equals this launch's (bounded spin, s_sleep between sweeps), and combines
-//      them in row-tile order -- the association of the split form's second kernel, so both
-//      forms give the same bits (the helpers below are shared and compiled without FMA
-//      contraction);
+//   2. after the GEMM, wave 0 stores its 16 columns' pairs as {a, tag, b, tag} granules, twice:
+//      a plain 16-B store into the `near` array (the line stays in this XCD's L2) and a
+//      write-through (sc1) 16-B store into the `slots` array (the line leaves L2 for the
+//      memory side: visible from every XCD), one 256-B run per workgroup each;
+//   3. wave 0 re-reads the R siblings' `near` entries of its column with sc1 loads (L1
+//      bypassed, served by its XCD's L2) until every tag equals this launch's, every 8th sweep
+//      the `slots` entries too (bounded spin, s_sleep between sweeps), and combines them in
+//      row-tile order -- the association of the split form's second kernel, so both forms give
+//      the same bits (the helpers below are shared and compiled without FMA contraction).
+//      A sibling on this XCD (the observed placement: siblings share blockIdx % 8) is read
+//      from L2 in ~0.2 us per sweep; the sc1 copy is what keeps a sibling on another XCD
+//      correct (its `near` line never reaches this L2), at the memory-side round trip
+//      (~1 us per sweep, the cost of every sweep when only the sc1 copy existed: 2.9 us from
+//      the last sibling's arrival to the end of the swap, tools/trace_train.py);
 //   4. the row-tile-0 workgroup of the column tile, once it has read every sibling's entry, adds
 //      1 to the tile's epoch word (agent atomic, no return).  Every sibling read that word before
 //      publishing, and row tile 0 adds only after it has seen all of them, so the word changes
@@ -77,7 +84,8 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 struct XchgSite {
   unsigned* epoch;   // per column tile one word, P3D_XCHG_EPOCH_STRIDE words apart
-  float* slots;      // [P3D_XCHG_MAXR row tiles][N columns] 16-B entries {a, tag, b, tag}
+  float* slots;      // [P3D_XCHG_MAXR row tiles][N columns] 16-B entries {a, tag, b, tag}, sc1-stored
+  float* near;       // the same entries, plain-stored (L2-resident on the producer's XCD)
   int* err;          // host-visible error word (pinned): 1 = a spin ran out
   int delay;         // test hook (env P3D_XCHG_TEST_DELAY): odd column tiles' last row tile sleeps
                      // ~delay x 3.4 us before reading its tag (a late-dispatched sibling)
@@ -91,30 +99,101 @@ __device__ __forceinline__ unsigned p3d_xchg_tag(const XchgSite& x, int ct, int 
   return __hip_atomic_load(x.epoch + ct * P3D_XCHG_EPOCH_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 }
 
-// Wave 0, all 64 lanes: lanes with `mine` publish their column's pair (write-through).
+// The publishing is done by ANOTHER wave than the polling one.  A wave's s_waitcnt vmcnt
+// covers its stores and loads together, in issue order: had the poller stored its own pair, each
+// of its sweeps would also wait for that write-through store to be acknowledged by the memory
+// side (~1 us), whatever the siblings' readiness.  So wave 0 posts its 16 pairs and the tag in
+// LDS (p3d_xchg_post), and wave 1 -- whose K slice is already combined and which would exit
+// otherwise -- stores them (p3d_xchg_publish) while wave 0 goes straight to its sweeps.
+struct XchgPub {
+  float a[16], b[16];
+  unsigned tag;      // 0 until wave 0 posts (wave 1 zeroes it before the K-combine barrier)
+};
+
+__device__ __forceinline__ void p3d_xchg_pub_reset(XchgPub* pub) {   // wave 1, before the barrier
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(&pub->tag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wave 0: lanes with q0 (one per column, lane i = column n0 + i) post their pair, then the tag
+__device__ __forceinline__ void p3d_xchg_post(XchgPub* pub, bool q0, int i, float a0, float b0, unsigned tag) {
+  if (q0) { pub->a[i] = a0; pub->b[i] = b0; }
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(&pub->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wave 1: wait for the post, store the 16 granules twice (plain: L2-resident near copy; sc1:
+// memory-side copy) for columns n0 .. n0 + 15 < N of row tile rt
+__device__ __forceinline__ void p3d_xchg_publish(const XchgSite& x, XchgPub* pub, int N, int rt, int n0) {
+  unsigned tag;
+  for (int spin = 0; (tag = __hip_atomic_load(&pub->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0; ++spin) {
+    if (spin > P3D_XCHG_SPIN) return;        // (wave 0 always posts)
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const int i = threadIdx.x & 63;
+#ifdef P3D_TRACE
+  const int tix = (n0 >> 4) + (N >> 4) * rt;
+  if (i == 0 && tix < 2048) g_p3d_trace[16384 + tix * 8 + 1] = wall_clock64();
+#endif
+  if (i < 16 && n0 + i < N) {
+    const u32x4_t v = {__float_as_uint(pub->a[i]), tag, __float_as_uint(pub->b[i]), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, p3d_rsrc(x.near), (rt * N + n0 + i) * 16, 0, 0);     // plain
+    __builtin_amdgcn_raw_buffer_store_b128(v, p3d_rsrc(x.slots), (rt * N + n0 + i) * 16, 0, 16);   // aux 16 = sc1
+  }
+#ifdef P3D_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (i == 0 && tix < 2048) g_p3d_trace[16384 + tix * 8 + 2] = wall_clock64();
+#endif
+}
+
+// Wave 0, all 64 lanes: lanes with `mine` publish their column's pair (one-wave form, WK = 1).
 __device__ __forceinline__ void p3d_xchg_put(const XchgSite& x, int N, int rt, int col, bool mine, float a0, float b0,
                                              unsigned tag) {
   if (mine) {
     const u32x4_t v = {__float_as_uint(a0), tag, __float_as_uint(b0), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, p3d_rsrc(x.near), (rt * N + col) * 16, 0, 0);     // plain
     __builtin_amdgcn_raw_buffer_store_b128(v, p3d_rsrc(x.slots), (rt * N + col) * 16, 0, 16);   // aux 16 = sc1
   }
 }
 
 // Wave 0, all 64 lanes: every lane collects the R pairs of column `col` (a[t], b[t], t < R)
 // once all R tags match (independent work of the caller can sit between put and get).
-__device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, int col, unsigned tag,
-                                             float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR]) {
-  const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(x.slots);
+// NR: a compile-time bound on R.  Every sweep issues its NR loads unconditionally (entries past
+// R re-read entry R - 1) and only then tests them: a load behind a runtime `t < R` branch made the
+// compiler wait for each load on its own (vmcnt(0) per entry: R dependent round trips per sweep,
+// ~3 us per exchange at R = 4), a straight run waits once per sweep.
+template <int NR>
+__device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, int col, unsigned tag,
+                                               float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR], int trace_rt) {
+  const __amdgpu_buffer_rsrc_t rn = p3d_rsrc(x.near), rs = p3d_rsrc(x.slots);
+#ifdef P3D_TRACE
+  const int tix = (col >> 4) + (N >> 4) * trace_rt;
+  if ((threadIdx.x & 63) == 0 && tix < 2048) g_p3d_trace[16384 + tix * 8 + 0] = wall_clock64();
+  int sweeps = 0, far = 0;
+#else
+  (void)trace_rt;
+#endif
+  bool got[NR];
+#pragma unroll
+  for (int t = 0; t < NR; ++t) got[t] = t >= R;
   for (int spin = 0;; ++spin) {
+    const bool far_sweep = (spin & 7) == 7;   // every 8th sweep: a sibling on another XCD (sc1 copy)
+    const __amdgpu_buffer_rsrc_t rr = far_sweep ? rs : rn;
+    u32x4_t v[NR];
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+      v[t] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, ((t < R ? t : R - 1) * N + col) * 16, 0, 16));
     bool ok = true;
 #pragma unroll
-    for (int t = 0; t < P3D_XCHG_MAXR; ++t)
-      if (t < R) {
-        const u32x4_t v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (t * N + col) * 16, 0, 16));
-        a[t] = __uint_as_float(v.x);
-        b[t] = __uint_as_float(v.z);
-        ok &= (v.y == tag) & (v.w == tag);
-      }
+    for (int t = 0; t < NR; ++t) {
+      const bool hit = !got[t] & (v[t].y == tag) & (v[t].w == tag);
+      a[t] = hit ? __uint_as_float(v[t].x) : a[t];
+      b[t] = hit ? __uint_as_float(v[t].z) : b[t];
+      got[t] = got[t] | hit;
+      ok &= got[t];
+    }
+#ifdef P3D_TRACE
+    ++sweeps;
+    far += far_sweep;
+#endif
     if (__all(ok)) break;
     if (spin > P3D_XCHG_SPIN) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -122,6 +201,19 @@ __device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, in
     }
     __builtin_amdgcn_s_sleep(1);
   }
+#ifdef P3D_TRACE
+  if ((threadIdx.x & 63) == 0 && tix < 2048) {
+    g_p3d_trace[16384 + tix * 8 + 3] = wall_clock64();
+    g_p3d_trace[16384 + tix * 8 + 4] = sweeps;
+    g_p3d_trace[16384 + tix * 8 + 5] = far;
+  }
+#endif
+}
+
+__device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, int col, unsigned tag,
+                                             float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR], int trace_rt = 0) {
+  if (R <= 4) p3d_xchg_get_n<4>(x, N, R, col, tag, a, b, trace_rt);     // B <= 64 (wave-uniform branch)
+  else p3d_xchg_get_n<P3D_XCHG_MAXR>(x, N, R, col, tag, a, b, trace_rt);
 }
 
 // Row tile 0 of column tile ct, after its swap: the tile's next launch gets a new tag.

@@ -402,6 +402,59 @@ def bench_serve(args, rank, world):
     return value, dt, roof
 
 
+def bench_latency_b64(reps=300):
+    """Launch-to-result latency of ONE batch-64 request (the reference's per-batch
+    step(isTraining=False), src/linear_model.py:239-245, device-resident input): host wall time
+    of issue + completion (torch.cuda.synchronize) per request, median over `reps`, and the
+    device time of the kernels (dispatch-attached events), for (a) p3d_serve at B = 64 (one
+    persistent launch, k_serve6 on 64 rows) and (b) the six-launch chain (p3d_forward, B = 64),
+    eager and as one replayed HIP graph."""
+    import torch
+    model, _ = make_model(data_parallel=False, max_batch=BATCH)
+    x = torch.from_numpy(np.random.default_rng(11).standard_normal((BATCH, IN)).astype(np.float32)).cuda()
+    y = torch.empty((BATCH, OUT), dtype=torch.float32, device="cuda")
+    flop = float(BATCH * flops_per_pose())
+    serve = model.serve_launcher(x, y)
+    chain = lambda: model.forward_device(x, False, 1.0, out=y, ctr=0)   # noqa: E731
+    chain()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=s0):
+        chain()
+    torch.cuda.current_stream().wait_stream(s0)
+    out = {"workload": "one batch-64 request (cfg2, BN eval, keep 1), input resident in HBM, launch to result",
+           "flop_per_request": int(flop)}
+    for name, fn in (("serve", serve), ("chain", chain), ("chain_graph", g.replay)):
+        for _ in range(30):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        prof = profile_kernels(model, lambda: [fn() for _ in range(50)]) if name != "chain_graph" else {}
+        dev = sum(v[0] * v[1] for v in prof.values()) / 50.0 if prof else None
+        ent = {"median_us": round(1e6 * ts[len(ts) // 2], 2), "p10_us": round(1e6 * ts[len(ts) // 10], 2),
+               "p90_us": round(1e6 * ts[(9 * len(ts)) // 10], 2)}
+        if dev:
+            ach = flop / (dev * 1e-6) / 1e12
+            ent["device_us"] = round(dev, 2)
+            ent["kernels_us"] = {k: round(v[1], 3) for k, v in prof.items()}
+            ent["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4)}
+        out[name] = ent
+    out["serve"]["kernel"] = kernel_name(model, 3)
+    model.serve_check()
+    del g
+    model.close()
+    return out
+
+
 def bench_infer(args, rank, world):
     """K forward steps of one 64-pose batch each.  S streams (one per hardware queue) each
     replay their own HIP graph of G/S steps over a disjoint workspace slot
@@ -1029,13 +1082,17 @@ def main():
         raise SystemExit("bench.py: --gpus %d but the job has %s rank(s) (WORLD_SIZE)"
                          % (args.gpus, os.environ.get("WORLD_SIZE", "1")))
     rank, world, local = setup_dist()
-    train = single = sweep = api = data = stress = None
+    train = single = sweep = api = data = stress = lat = None
     chain = None
     if args.mode == "infer":
         value, dt, roof = bench_serve(args, rank, world)
-        workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1, batch 64 per step; "
-                    "p3d_serve persistent launches of %d steps, whole network per XCD"
-                    % roof["steps_per_launch"])
+        workload = ("cfg2 inference: L=1024, 2 residual blocks, BN(eval), keep=1; a step = one batch-64 request "
+                    "(its own 64 poses); %d requests per persistent p3d_serve launch (%d rows, whole network "
+                    "per XCD); one request alone: latency_b64" % (roof["steps_per_launch"], 64 * roof["steps_per_launch"]))
+        try:
+            lat = bench_latency_b64()
+        except Exception as exc:
+            lat = {"error": repr(exc)[:300]}
         if not args.no_streams:   # the per-step kernel chain (six launches per step), 4 streams
             try:
                 cv, cdt, croof, single = bench_infer(args, rank, world)
@@ -1144,6 +1201,8 @@ def main():
                            {"workload": workload, "global_batch": 1024 * world, "linear_size": 4096,
                             "num_layers": 4, "parallelism": "dp%d" % world}),
                 "roofline": roof, "cpu_baseline": cpu}
+        if lat is not None:
+            line["latency_b64"] = lat
         if chain is not None:
             line["stream_chain"] = chain
         if single is not None:

@@ -45,3 +45,17 @@ print("sibling skew of 'reduced' (max-min over the 4 row tiles): med %.2f max %.
       % (np.median(g.max(0) - g.min(0)), (g.max(0) - g.min(0)).max()))
 print("exchange done - latest sibling reduced: med %.2f max %.2f us"
       % (np.median(b - g.max(0)), (b - g.max(0)).max()))
+x = buf.reshape(4096, 8)[:nwg, 7].astype(np.int64).reshape(4, gx)     # hardware XCD id per workgroup
+same = (x == x[0:1]).all(0)
+print("column tiles whose 4 row-tile siblings share an XCD: %d / %d" % (int(same.sum()), gx))
+e = buf[16384:16384 + nwg * 8].astype(np.int64).reshape(nwg, 8)   # exchange detail (the last exchange launch)
+t0 = e[:, 0].min() - 300   # (its own time base: the first get start, minus 3 us)
+us = lambda v: (v - t0) * 10.0 / 1000.0   # noqa: E731
+for k, n in ((0, "get start (w0)"), (1, "publish issue (w1)"), (2, "publish acked (w1)"), (3, "get done (w0)")):
+    d = us(e[:, k])
+    print("%-20s min %6.2f  med %6.2f  max %6.2f us" % (n, d.min(), np.median(d), d.max()))
+print("sweeps per get: med %d max %d; memory-side sweeps med %d max %d"
+      % (np.median(e[:, 4]), e[:, 4].max(), np.median(e[:, 5]), e[:, 5].max()))
+pa = us(e[:, 2]).reshape(4, gx).max(0)         # the latest sibling's publish acked
+print("get done - latest sibling acked: med %.2f max %.2f us"
+      % (np.median(us(e[:, 3]).reshape(4, gx) - pa), (us(e[:, 3]).reshape(4, gx) - pa).max()))
