@@ -1081,6 +1081,11 @@ def main():
     if args.gpus != int(os.environ.get("WORLD_SIZE", "1")):
         raise SystemExit("bench.py: --gpus %d but the job has %s rank(s) (WORLD_SIZE)"
                          % (args.gpus, os.environ.get("WORLD_SIZE", "1")))
+    # everything the libraries print (RCCL's banner at communicator creation, ...) goes to
+    # stderr: stdout carries exactly the one JSON line
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     rank, world, local = setup_dist()
     train = single = sweep = api = data = stress = lat = None
     chain = None
@@ -1219,7 +1224,8 @@ def main():
             line["stress"] = stress
         if cfg1 is not None:
             line["cfg1"] = cfg1
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
