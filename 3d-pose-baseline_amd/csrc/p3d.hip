@@ -2469,9 +2469,11 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
 struct Serve6Plan { int S = 0, rt = 4, ncm = 0; };
 
 // the built (RT, NCM) forms: batch-64 units with 2 / 4 / 7 / 8 column tiles per CU, half-step
-// units with 11, and XCD-wide units (S = 1, 2 tiles per CU) of 6 .. 16 row tiles
+// units with 11 (S = 5) or 2 (S = 1), 16-row units with 2 (S = 1: a lone batch-64 request on
+// four XCDs), and XCD-wide units (S = 1, 2 tiles per CU) of 6 .. 16 row tiles
 static int serve6_ncm_for(int rt, int need) {
-  if (rt == 2) return need <= 11 ? 11 : 0;
+  if (rt == 1) return need <= 2 ? 2 : 0;
+  if (rt == 2) return need <= 2 ? 2 : need <= 11 ? 11 : 0;
   if (rt == 4) return need <= 2 ? 2 : need <= 4 ? 4 : need <= 7 ? 7 : need <= 8 ? 8 : 0;
   return need <= 2 ? 2 : 0;
 }
@@ -2481,16 +2483,19 @@ static int serve6_ncm_for(int rt, int need) {
 // epilogue) ~4 us, a column tile of K = 1024 ~3.9 us at 4 row tiles, proportional to the row
 // tiles (round-1 phase traces).  20 batch-64 steps (1280 rows): RT = 10, S = 1 --
 // 160 rows per XCD, 2 column tiles per CU (the half-step form, RT = 2 with 5 groups per XCD,
-// costs 11 tiles of 2 row tiles per CU: 22 vs 20 tile-units and 5x the weight reads).
+// costs 11 tiles of 2 row tiles per CU: 22 vs 20 tile-units and 5x the weight reads).  A
+// wide form (NCM >= 7) is priced at its full width: its register ring and epilogue run NCM
+// tiles whatever share of them a member owns.  One batch-64 request: RT = 1, four 16-row units
+// on four XCDs, 2 tiles per CU (vs one XCD at RT = 4).
 static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
-  static const int rts[] = {4, 2, 6, 8, 10, 12, 16};
+  static const int rts[] = {4, 2, 1, 6, 8, 10, 12, 16};
   const int cx = std::max(1, m->serve_grid / 8);
   const double cfix = 4.0;
   Serve6Plan best;
   double bt = 1e30;
   for (int rt : rts) {
     if (m->serve6_rt && m->serve6_rt != rt) continue;
-    if (rt > 4 && (T / 4) % 4 != 0) continue;   // the XCD-wide forms run a 4-deep weight ring
+    if ((rt > 4 || rt == 1) && (T / 4) % 4 != 0) continue;   // these forms run a 4-deep weight ring
     const int64_t nb = (B + 16 * rt - 1) / (16 * rt);
     const double ctile = 3.9 * (rt / 4.0) * T / 64.0;
     for (int S = 1; S <= 8; ++S) {
@@ -2500,7 +2505,8 @@ static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
       const int need = (T + nmin - 1) / nmin, ncm = serve6_ncm_for(rt, need);
       if (!ncm || need > (ncm >= 7 ? ncm : 2 * ncm)) continue;
       const double rounds = (double)((nb + 8 * S - 1) / (8 * S));
-      const double t = rounds * (cfix + ctile * need);
+      if (rt == 2 && ncm == 2 && (T / 4) % 4 != 0) continue;
+      const double t = rounds * (cfix + ctile * (ncm >= 7 ? ncm : need));
       if (t < bt - 1e-9) { bt = t; best.S = S; best.rt = rt; best.ncm = ncm; }
     }
   }
@@ -2510,7 +2516,11 @@ static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
 static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, int rt, unsigned grid,
                           hipStream_t st, const ServeArgs& a) {
   switch (rt) {   // half-step units (11 column tiles, S = 5) / XCD-wide units (2 tiles, S = 1)
-    case 2: go(ps, k_serve6<2, 3, 11, 2>, dim3(grid), dim3(256), st, a); return;
+    case 1: go(ps, k_serve6<4, 3, 2, 1>, dim3(grid), dim3(256), st, a); return;
+    case 2:
+      if (ncm == 2) go(ps, k_serve6<4, 3, 2, 2>, dim3(grid), dim3(256), st, a);
+      else go(ps, k_serve6<2, 3, 11, 2>, dim3(grid), dim3(256), st, a);
+      return;
     case 6: go(ps, k_serve6<4, 3, 2, 6>, dim3(grid), dim3(256), st, a); return;
     case 8: go(ps, k_serve6<4, 3, 2, 8>, dim3(grid), dim3(256), st, a); return;
     case 10: go(ps, k_serve6<4, 3, 2, 10>, dim3(grid), dim3(256), st, a); return;
@@ -2630,7 +2640,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     const int T = L / 16;
     const int ncm = plan.ncm;
     int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
-    if (plan.rt == 2) depth = 2;
+    if (plan.rt == 2) depth = ncm == 2 ? 4 : 2;
+    if (plan.rt == 1) depth = 4;
     if (plan.rt > 4) depth = 4;   // (an 8-deep weight ring measured 117 vs 107-112 us at RT = 10)
     m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ", " +
                      std::to_string(plan.rt) + ">";

@@ -59,9 +59,13 @@
 // of group g
 #define P3D_SERVE_FLAG0 256
 #define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 64)   // flags of up to 64 groups (k_serve6 S <= 8)
-// the model's serve sync allocation: k_serve6 banks 0 / 1, the k_serve5 bank, then k_serve6's
-// device epoch word (bank = epoch & 1) on a line of its own
-#define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 64)
+// the model's serve sync allocation: k_serve6 banks 0 / 1 (group flags), the k_serve5 bank, then
+// k_serve6's device epoch word (bank = epoch & 1) on a line of its own, its census counters C[x]
+// (arrivals on XCD x over all launches, never reset) and their bases B[x] (C[x] at the end of the
+// previous launch's census), each on a 128-B line of its own
+#define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 32 + 512)
+#define P3D_SERVE_CENSUS_C 32          // word offsets from the epoch word
+#define P3D_SERVE_CENSUS_B (32 + 256)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int ECT = NCM >= 7 ? NCM : 2 * NCM;
   __shared__ __attribute__((aligned(16))) float ec[(P3D_SERVE_MAXL - 1) * ECT * 48];
   __shared__ float ecm[P3D_SERVE_MAXL];
-  __shared__ int sh[20];
+  __shared__ int sh[32];
   // wave-uniform values the compiler cannot prove uniform (the wave index, everything read
   // from the census in LDS) go through readfirstlane: they end in scalar registers, and
   // buffer loads with a scalar offset need no per-lane waterfall loop
@@ -125,23 +125,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // The sync words come in two banks used by alternate launches, picked by the device epoch
   // word: this launch zeroes the other bank for the next one (stream order: the launch that
   // used it has completed), so a launch needs no memset in front of it
+  // Arrival in ONE memory round trip: the epoch read, the returning add on this XCD's census
+  // counter C[x] and the reads of the launch's census bases B[0..7] are in flight together (the
+  // counters are never reset: this launch's rank on XCD x is the add's old value - B[x], its
+  // count there C[x] - B[x]).  Were the counters in the epoch's bank, the arrival would wait for
+  // the epoch first: two dependent round trips to the memory side (~1 us each) before the wait.
+  unsigned* const censc = p.epoch + P3D_SERVE_CENSUS_C;
+  unsigned* const censb = p.epoch + P3D_SERVE_CENSUS_B;
   if (tid == 0) {
-    sh[3] = (int)(__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u);
+    unsigned xr;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+    const int xc = (int)(xr & 7u);
+    const unsigned ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(censc + 32 * xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned bs[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) bs[x] = __hip_atomic_load(censb + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = xc;
+    sh[1] = (int)(old - bs[xc]);
+    sh[3] = (int)(ep & 1u);
     sh[4] = 0;                               // some wave of this workgroup is broken (group_sync)
+#pragma unroll
+    for (int x = 0; x < 8; ++x) sh[24 + x] = (int)bs[x];
   }
   __syncthreads();
+#ifdef P3D_TRACE
+  if (tid == 0 && blockIdx.x < 1024) {     // per workgroup: start, arrival, census end, XCD | rank
+    g_p3d_trace[16384 + blockIdx.x * 4 + 0] = t_start;
+    g_p3d_trace[16384 + blockIdx.x * 4 + 1] = wall_clock64();
+    g_p3d_trace[16384 + blockIdx.x * 4 + 3] = (unsigned long long)(sh[0] | (sh[1] << 8));
+  }
+#endif
   const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
   unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
   {
     unsigned* other = p.sync + (bank ^ 1) * P3D_SERVE_SYNC_WORDS;
     for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
   }
-  // The census in two halves: after its arrival (XCD id, rank) a workgroup guesses its place
-  // assuming every XCD holds grid / 8 workgroups (the dispatcher's round-robin) and requests its
-  // first input-layer operands and epilogue constants; the wait for every workgroup's arrival
-  // then hides their latency.  The guess is used only if the final counts confirm it (every
-  // workgroup sees the same counts, so all decide alike); otherwise the loads are re-issued.
-  p3d_serve_census_arrive(sync, sh);
+  // After its arrival (XCD id, rank) a workgroup guesses its place assuming every XCD holds
+  // grid / 8 workgroups (the dispatcher's round-robin) and requests its first input-layer
+  // operands and epilogue constants; the wait for every workgroup's arrival then hides their
+  // latency.  The guess is used only if the final counts confirm it (every workgroup sees the
+  // same counts, so all decide alike); otherwise the loads are re-issued.
   const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
   constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
   // place of this workgroup for XCD counts cnt(x): member r of group gid (gi-th of ng groups
@@ -203,7 +228,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     place([&](int) { return nxg; }, xcc, rx, g_r, g_n, g_gid, g_gi, g_ng);
     prefetch(g_gi, (T * g_r) / g_n, (T * (g_r + 1)) / g_n);
   }
-  p3d_serve_census_wait(p, sync, sh, (S < 1 || S > 8) ? -1 : 64 * S);
+  if (tid == 0) {   // the wait: every workgroup arrived (this launch's counts C[x] - B[x] sum to the grid)
+    const int maxn = (S < 1 || S > 8) ? -1 : 64 * S;
+    int bad = 0, spin = 0;
+    unsigned c[8];
+    const unsigned expect = gridDim.x + (unsigned)p.census_extra;
+    while (true) {
+      unsigned tot = 0;
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        c[x] = __hip_atomic_load(censc + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)sh[24 + x];
+        tot += c[x];
+      }
+      if (tot >= expect) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
+    }
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      sh[8 + x] = (int)c[x];
+      if ((int)c[x] > maxn) bad = 1;   // judged on every XCD's count: all workgroups decide alike
+    }
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sh[2] = bad;
+  }
+  __syncthreads();
+#ifdef P3D_TRACE
+  if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[16384 + blockIdx.x * 4 + 2] = wall_clock64();
+#endif
   if (sh[2]) {
     // the census failed (not every workgroup resident within the bounded wait): no row of this
     // launch is computed; each workgroup fills a stripe of the output with NaN, so a caller who
@@ -212,12 +264,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float qnan = __builtin_nanf("");
     for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < p.M * p.ND; e += (int64_t)gridDim.x * 256) p.y[e] = qnan;
   } else {
-  // every workgroup has read the epoch (before arriving): one of them advances it for the next
-  // launch -- rank 0 of the lowest-numbered XCD that holds workgroups (all see the same counts)
+  // One workgroup -- rank 0 of the lowest-numbered XCD that holds workgroups (all see the same
+  // counts) -- advances the epoch and moves the bases to the final counters for the next launch,
+  // at the END of its work: the epoch and base reads of the others were issued together with
+  // their arrivals (not ahead of them), so an update right after the census could overtake a read
+  // still in flight; a launch's length later every read has long returned (a wave's memory
+  // requests complete in bounded time -- a context-saved wave drains them first).
+  bool leader = false;
   if (tid == 0 && sh[1] == 0) {
     int lead = 0;
     while (lead < 7 && sh[8 + lead] == 0) ++lead;
-    if (sh[0] == lead) __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    leader = sh[0] == lead;
   }
   bool guess_held = guessable;
 #pragma unroll
@@ -626,6 +683,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #ifdef P3D_TRACE
     if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
+  }
+  if (leader) {
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+      __hip_atomic_store(censb + 32 * x, (unsigned)sh[24 + x] + (unsigned)sh[8 + x], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   }
 }

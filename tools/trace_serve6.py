@@ -62,6 +62,18 @@ def main():
     for d in out:
         print(json.dumps(d))
     print("launch end (latest reduce): %.2f us" % max(d["reduce_end"] for d in out))
+    # every workgroup's start / arrival / census end (the dispatch ramp)
+    wg = buf[16384:16384 + 4 * 1024].astype(np.int64).reshape(1024, 4)
+    wg = wg[(wg[:, 0] >= t0) & (wg[:, 2] >= wg[:, 0])]
+    if len(wg):
+        st = np.sort((wg[:, 0] - t0) / 100.0)
+        ar = np.sort((wg[:, 1] - t0) / 100.0)
+        ce = (wg[:, 2] - t0) / 100.0
+        q = lambda a: [round(float(np.quantile(a, f)), 2) for f in (0, 0.25, 0.5, 0.75, 0.9, 1.0)]  # noqa: E731
+        print(json.dumps({"workgroups": len(wg), "start_q": q(st), "arrive_q": q(ar), "census_end_q": q(ce),
+                          "arrive_minus_start_q": q((wg[:, 1] - wg[:, 0]) / 100.0),
+                          "per_xcd_last_start": [round(float(((wg[(wg[:, 3] & 255) == x, 0] - t0) / 100.0).max()), 2)
+                                                 if ((wg[:, 3] & 255) == x).any() else None for x in range(8)]}))
 
 
 if __name__ == "__main__":
