@@ -7,10 +7,20 @@
   ``unNormalizeData`` (:283-311), ``transform_world_to_camera`` (:233-257),
   ``project_to_cameras`` (:339-364) and ``postprocess_3d`` (:474-494).  Each batches all the
   sequences of a subject into one launch.
-* The HDF5 loaders (``load_data``, ``load_stacked_hourglass``, ``read_*``) read the H3.6M
-  files, which are not in the image: out of scope.
+* The loaders ``load_data`` (:61-117), ``load_stacked_hourglass`` (:120-192) and the
+  pipelines ``read_3d_data`` (:431-471), ``create_2d_data`` (:395-428) and
+  ``read_2d_predictions`` (:367-392) read the H3.6M tree either as the reference's directory of
+  HDF5 files (needs h5py, which this image lacks) or as ONE ``.npz`` archive whose member names
+  are the tree's relative paths (``S1/MyPoses/3D_positions/Walking 1.h5`` holding the file's
+  dataset as stored, e.g. [96, n]) -- the same files, sequence names, selection rules and
+  counts; the numeric stages above run on the GPU.
 """
 from __future__ import annotations
+
+import copy
+import fnmatch
+import glob
+import os
 
 import numpy as np
 
@@ -147,3 +157,139 @@ def postprocess_3d(poses_set):
         poses_set[k] = centred[off:off + n]
         off += n
     return poses_set, roots
+
+
+# ---- the H3.6M tree: an npz archive of its files, or the directory itself ----------------
+class _Tree:
+    """Files of the H3.6M tree under ``bpath`` by relative path: an ``.npz`` archive (member
+    name = relative path of the file, value = the file's dataset) or a directory of the
+    reference's HDF5 files (h5py)."""
+
+    def __init__(self, bpath):
+        self.bpath = bpath
+        self.npz = None
+        if os.path.isfile(bpath):
+            self.npz = np.load(bpath, allow_pickle=False)
+            self.names = list(self.npz.files)
+
+    def glob(self, pattern):
+        """Relative paths matching ``pattern`` (glob semantics on the archive's names; the
+        reference's glob.glob on a directory)."""
+        if self.npz is None:
+            base = os.path.join(self.bpath, "")
+            return [f[len(base):] if f.startswith(base) else f
+                    for f in glob.glob(os.path.join(self.bpath, pattern))]
+        d, leaf = os.path.split(pattern)
+        return [n for n in self.names if os.path.dirname(n) == d and fnmatch.fnmatchcase(os.path.basename(n), leaf)]
+
+    def read(self, rel, dataset):
+        if self.npz is not None:
+            return np.asarray(self.npz[rel])
+        try:
+            import h5py
+        except ImportError as e:   # the image has no h5py: the archive form is the supported one
+            raise ImportError("reading the H3.6M HDF5 files needs h5py; pass the tree as an .npz archive "
+                              "(data_utils module docstring)") from e
+        with h5py.File(os.path.join(self.bpath, rel), "r") as h5f:
+            return h5f[dataset][:]
+
+
+def load_data(bpath, subjects, actions, dim=3):
+    """{(subject, action, seqname): [n, 32 * dim]} from ``S<subj>/MyPoses/<dim>D_positions/<action>*.h5``
+    (src/data_utils.py:61-117): the same Sitting / SittingDown and prefix rules, 2 sequences per
+    subject and action for 3D, 8 for 2D."""
+    if dim not in (2, 3):
+        raise ValueError('dim must be 2 or 3')
+    tree = _Tree(bpath)
+    data = {}
+    for subj in subjects:
+        for action in actions:
+            names = tree.glob(os.path.join('S{0}'.format(subj), 'MyPoses/{0}D_positions'.format(dim),
+                                           '{0}*.h5'.format(action)))
+            loaded = 0
+            for rel in names:
+                seqname = os.path.basename(rel)
+                if action == "Sitting" and seqname.startswith("SittingDown"):
+                    continue
+                if seqname.startswith(action):
+                    loaded += 1
+                    data[(subj, action, seqname)] = tree.read(rel, '{0}D_positions'.format(dim)).T
+            want = 8 if dim == 2 else 2
+            assert loaded == want, "Expecting {0} sequences, found {1} instead".format(want, loaded)
+    return data
+
+
+# Stacked Hourglass joint order -> H3.6M (src/data_utils.py:134-135)
+SH_TO_GT_PERM = np.array([SH_NAMES.index(h) for h in H36M_NAMES if h != '' and h in SH_NAMES])
+
+
+def load_stacked_hourglass(data_dir, subjects, actions):
+    """{(subject, action, seqname + '-sh'): [n, 64]} from ``S<subj>/StackedHourglass/<action>*.h5``
+    (src/data_utils.py:120-192): detections permuted to H3.6M order and scattered into the 64
+    2D columns; 8 sequences per subject and action (7 for S11 Directions)."""
+    tree = _Tree(data_dir)
+    xs = np.flatnonzero(np.array([x != '' and x != 'Neck/Nose' for x in H36M_NAMES])) * 2
+    cols = np.zeros(len(SH_NAMES) * 2, dtype=np.int32)
+    cols[0::2], cols[1::2] = xs, xs + 1
+    data = {}
+    for subj in subjects:
+        for action in actions:
+            names = tree.glob(os.path.join('S{0}'.format(subj), 'StackedHourglass/{0}*.h5'.format(action)))
+            loaded = 0
+            for rel in names:
+                seqname = os.path.basename(rel).replace('_', ' ')
+                if action == "Sitting" and seqname.startswith("SittingDown"):
+                    continue
+                if seqname.startswith(action):
+                    loaded += 1
+                    poses = tree.read(rel, 'poses')[:, SH_TO_GT_PERM, :]
+                    poses = np.reshape(poses, [poses.shape[0], -1])
+                    final = np.zeros([poses.shape[0], len(H36M_NAMES) * 2])
+                    final[:, cols] = poses
+                    data[(subj, action, seqname + '-sh')] = final
+            want = 7 if (subj == 11 and action == 'Directions') else 8
+            assert loaded == want, "Expecting {0} sequences, found {1} instead. S:{2} {3}".format(
+                want, loaded, subj, action)
+    return data
+
+
+def read_3d_data(actions, data_dir, camera_frame, rcams, predict_14=False):
+    """3D poses: (optionally) into every camera's frame, root-centred, normalised with the
+    training set's statistics (src/data_utils.py:431-471).  Returns train_set, test_set,
+    data_mean, data_std, dim_to_ignore, dim_to_use, train_root_positions, test_root_positions."""
+    train_set = load_data(data_dir, TRAIN_SUBJECTS, actions, dim=3)
+    test_set = load_data(data_dir, TEST_SUBJECTS, actions, dim=3)
+    if camera_frame:
+        train_set = transform_world_to_camera(train_set, rcams)
+        test_set = transform_world_to_camera(test_set, rcams)
+    train_set, train_root_positions = postprocess_3d(train_set)
+    test_set, test_root_positions = postprocess_3d(test_set)
+    complete_train = copy.deepcopy(np.vstack(list(train_set.values())))
+    data_mean, data_std, dim_to_ignore, dim_to_use = normalization_stats(complete_train, dim=3,
+                                                                         predict_14=predict_14)
+    train_set = normalize_data(train_set, data_mean, data_std, dim_to_use)
+    test_set = normalize_data(test_set, data_mean, data_std, dim_to_use)
+    return (train_set, test_set, data_mean, data_std, dim_to_ignore, dim_to_use, train_root_positions,
+            test_root_positions)
+
+
+def _normalized_2d(train_set, test_set):
+    complete_train = copy.deepcopy(np.vstack(list(train_set.values())))
+    data_mean, data_std, dim_to_ignore, dim_to_use = normalization_stats(complete_train, dim=2)
+    train_set = normalize_data(train_set, data_mean, data_std, dim_to_use)
+    test_set = normalize_data(test_set, data_mean, data_std, dim_to_use)
+    return train_set, test_set, data_mean, data_std, dim_to_ignore, dim_to_use
+
+
+def create_2d_data(actions, data_dir, rcams):
+    """2D inputs: the 3D poses projected into every camera, normalised with the training set's
+    statistics (src/data_utils.py:395-428)."""
+    train_set = project_to_cameras(load_data(data_dir, TRAIN_SUBJECTS, actions, dim=3), rcams)
+    test_set = project_to_cameras(load_data(data_dir, TEST_SUBJECTS, actions, dim=3), rcams)
+    return _normalized_2d(train_set, test_set)
+
+
+def read_2d_predictions(actions, data_dir):
+    """2D inputs from the Stacked Hourglass detections (src/data_utils.py:367-392)."""
+    return _normalized_2d(load_stacked_hourglass(data_dir, TRAIN_SUBJECTS, actions),
+                          load_stacked_hourglass(data_dir, TEST_SUBJECTS, actions))

@@ -12,8 +12,9 @@ the epoch ``train`` loop (:188-334), ``get_action_subset`` (:337-349) and
 * ``evaluate_action_wise`` shards each action's batches across the ranks of a
   ``torch.distributed`` job and combines per-action sums with one RCCL
   all-reduce (SURVEY.md 8e);
-* the H3.6M loaders are not part of this build: ``--synthetic`` feeds data of
-  the reference's shapes.
+* the H3.6M tree and cameras.h5 are read as the reference's HDF5 files (h5py) or as .npz
+  archives of the same datasets under the same paths (``load_data``); ``--synthetic`` feeds
+  data of the reference's shapes without files.
 """
 from __future__ import annotations
 
@@ -25,6 +26,7 @@ import time
 import numpy as np
 
 import _p3d
+import cameras
 import data_utils
 import dist_utils
 import linear_model
@@ -337,11 +339,30 @@ def dp_epoch_share(enc, dec, rank, world):
     return enc[rank * per:(rank + 1) * per], dec[rank * per:(rank + 1) * per]
 
 
+SUBJECT_IDS = [1, 5, 6, 7, 8, 9, 11]
+
+
 def load_data(flags):
+    """The training / test sets and their statistics (src/predict_3dpose.py:194-208): cameras,
+    3D poses (camera frame, root-centred, normalised) and the 2D inputs -- ground-truth
+    projections or Stacked Hourglass detections.  ``--data_dir`` / ``--cameras_path`` name the
+    H3.6M tree and cameras.h5 or their .npz archives (data_utils, cameras); ``--synthetic``
+    skips the files."""
     if flags.synthetic:
         return synthetic_h36m(out_dim=42 if flags.predict_14 else 48, seed=flags.seed)
-    raise NotImplementedError("H3.6M loaders (read_3d_data / read_2d_predictions) are not part of this "
-                              "build; pass --synthetic or feed normalized arrays to LinearModel.step")
+    actions = data_utils.define_actions(flags.action)
+    rcams = cameras.load_cameras(flags.cameras_path, SUBJECT_IDS)
+    (train_set_3d, test_set_3d, data_mean_3d, data_std_3d, dim_to_ignore_3d, dim_to_use_3d, _,
+     _) = data_utils.read_3d_data(actions, flags.data_dir, flags.camera_frame, rcams, flags.predict_14)
+    if flags.use_sh:
+        two = data_utils.read_2d_predictions(actions, flags.data_dir)
+    else:
+        two = data_utils.create_2d_data(actions, flags.data_dir, rcams)
+    train_set_2d, test_set_2d, data_mean_2d, data_std_2d, dim_to_ignore_2d, dim_to_use_2d = two
+    return dict(train_set_2d=train_set_2d, train_set_3d=train_set_3d, test_set_2d=test_set_2d,
+                test_set_3d=test_set_3d, data_mean_3d=data_mean_3d, data_std_3d=data_std_3d,
+                dim_to_use_3d=dim_to_use_3d, dim_to_ignore_3d=dim_to_ignore_3d, data_mean_2d=data_mean_2d,
+                data_std_2d=data_std_2d, dim_to_use_2d=dim_to_use_2d, dim_to_ignore_2d=dim_to_ignore_2d)
 
 
 def train(flags=None):

@@ -56,3 +56,43 @@ def synth_world_poses(rng, n, joints=32):
     off = rng.normal(0, 250, (1, joints, 3)) + rng.normal(0, 20, (n, joints, 3))
     off[:, 0] = 0.0
     return (root[:, None, :] + off).reshape(n, joints * 3)
+
+
+def write_h36m_archives(tree_path, cams_path, rng, actions, frames=120, subjects=(1, 5, 6, 7, 8, 9, 11),
+                        sh=False, decoys=True):
+    """Synthetic H3.6M tree and cameras as .npz archives (member name = the file's relative path
+    in the reference's tree / the dataset path in cameras.h5, value = the dataset as stored:
+    3D_positions [96, n], StackedHourglass poses [n, 16, 2], R transposed, Name as character
+    codes).  Two 3D sequences per subject and action ("<action> 1.h5", "<action>.h5"); with
+    ``sh`` the 8 Stacked Hourglass files (7 for S11 Directions); ``decoys`` adds files the
+    reference's selection rules must skip (SittingDown under Sitting, other actions).
+    Returns (rcams, {(subject, action, seqname): world poses [n, 96]})."""
+    cams, _, _ = synth_cameras(rng, subjects)
+    cz = {}
+    for (s, ci), (R, T, f, c, k, p, name) in cams.items():
+        pre = "subject%d/camera%d/" % (s, ci)
+        cz[pre + "R"] = R.T
+        cz[pre + "T"], cz[pre + "f"], cz[pre + "c"], cz[pre + "k"], cz[pre + "p"] = T, f, c, k, p
+        cz[pre + "Name"] = np.array([ord(ch) for ch in name], np.int64)
+    np.savez(cams_path, **cz)
+    tree, world = {}, {}
+    for s in subjects:
+        for a in actions:
+            for seq in ("%s 1.h5" % a, "%s.h5" % a):
+                P = synth_world_poses(rng, frames + int(rng.integers(0, 17)))
+                tree["S%d/MyPoses/3D_positions/%s" % (s, seq)] = P.T
+                world[(s, a, seq)] = P
+                if sh:
+                    for ci, cname in enumerate(CAM_NAMES):
+                        if s == 11 and a == "Directions" and seq == "%s.h5" % a and ci == 3:
+                            continue   # the reference's damaged video
+                        fn = (seq[:-3] + "." + cname + ".h5").replace(" ", "_")
+                        tree["S%d/StackedHourglass/%s" % (s, fn)] = rng.normal(500, 100, (len(P), 16, 2))
+            if decoys and a == "Sitting" and "SittingDown" not in actions:
+                tree["S%d/MyPoses/3D_positions/SittingDown 1.h5" % s] = synth_world_poses(rng, 5).T
+                if sh:
+                    tree["S%d/StackedHourglass/SittingDown_1.%s.h5" % (s, CAM_NAMES[0])] = rng.normal(0, 1, (5, 16, 2))
+        if decoys:
+            tree["S%d/MyPoses/2D_positions/%s" % (s, "Walking 1.h5")] = synth_world_poses(rng, 3)[:, :64].T
+    np.savez(tree_path, **tree)
+    return cams, world

@@ -169,3 +169,52 @@ def test_empty_inputs():
     assert data_utils.normalize_data({}, np.zeros(96), np.ones(96), np.arange(48)) == {}
     with pytest.raises(ValueError):
         dp.moments(np.zeros((0, 4)))
+
+
+def _oracle_norm(train, test, dim, predict_14=False):
+    from oracle import ref_eval
+    mean, std = ref_data.moments(np.vstack(list(train.values())))
+    use, ign = data_utils.dimension_sets(dim, predict_14)
+    f = lambda d: {k: (v[:, use] - mean[use]) / std[use] for k, v in d.items()}  # noqa: E731
+    return f(train), f(test), mean, std, ign, use
+
+
+@pytest.mark.parametrize("camera_frame", [True, False])
+def test_read_3d_and_create_2d_from_archives_vs_oracle(tmp_path, camera_frame):
+    """read_3d_data / create_2d_data (src/data_utils.py:395-471) over the .npz archive form of
+    the H3.6M tree: the files the reference would select, every stage on the GPU, against the
+    oracle's restatement of the same pipeline (transforms bit-exact, projections 1 ulp,
+    statistics 1e-12)."""
+    from synth_cameras import write_h36m_archives
+    rng = np.random.default_rng(21)
+    tree, camsp = str(tmp_path / "h36m.npz"), str(tmp_path / "cameras.npz")
+    actions = ["Sitting", "Walking"]
+    _, world = write_h36m_archives(tree, camsp, rng, actions, frames=300)
+    rcams = cameras.load_cameras(camsp, [1, 5, 6, 7, 8, 9, 11])
+    got = data_utils.read_3d_data(actions, tree, camera_frame, rcams)
+    wtr = {k: world[k] for k in world if k[0] in data_utils.TRAIN_SUBJECTS}
+    wte = {k: world[k] for k in world if k[0] in data_utils.TEST_SUBJECTS}
+    tr3 = ref_data.transform_world_to_camera(wtr, rcams) if camera_frame else wtr
+    te3 = ref_data.transform_world_to_camera(wte, rcams) if camera_frame else wte
+    tr3, rtr = ref_data.postprocess_3d(tr3)
+    te3, rte = ref_data.postprocess_3d(te3)
+    want = _oracle_norm(tr3, te3, 3)
+    for g, w in zip(got[:2], want[:2]):
+        assert sorted(g) == sorted(w)
+        for k in w:
+            np.testing.assert_allclose(g[k], w[k], rtol=1e-11, atol=1e-11, err_msg=str(k))
+    np.testing.assert_allclose(got[2], want[2], rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(got[3], want[3], rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(got[4], want[4])
+    np.testing.assert_array_equal(got[5], want[5])
+    for g, w in ((got[6], rtr), (got[7], rte)):
+        for k in w:
+            np.testing.assert_array_equal(g[k], w[k])
+    got2 = data_utils.create_2d_data(actions, tree, rcams)
+    want2 = _oracle_norm(ref_data.project_to_cameras(wtr, rcams), ref_data.project_to_cameras(wte, rcams), 2)
+    for g, w in zip(got2[:2], want2[:2]):
+        assert sorted(g) == sorted(w)
+        for k in w:
+            np.testing.assert_allclose(g[k], w[k], rtol=1e-11, atol=1e-11, err_msg=str(k))
+    np.testing.assert_allclose(got2[2], want2[2], rtol=1e-12)
+    np.testing.assert_allclose(got2[3], want2[3], rtol=1e-12)

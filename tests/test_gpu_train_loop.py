@@ -72,3 +72,34 @@ def test_create_model_load_restores_latest(tmp_path):
     with pytest.raises(ValueError, match="does not seem to exist"):
         bad = predict_3dpose.build_parser().parse_args(args + ["--load", str(s1 + 1)])
         predict_3dpose.create_model(None, ["All"], bad.batch_size, bad)
+
+
+@pytest.mark.parametrize("use_sh", [False, True])
+def test_train_from_archives(tmp_path, use_sh):
+    """train() on files (src/predict_3dpose.py:194-208): cameras, 3D poses and 2D inputs read
+    from the .npz archive forms of cameras.h5 and the H3.6M tree through data_utils'
+    read_3d_data / create_2d_data (or read_2d_predictions), one epoch, evaluation, checkpoint."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from synth_cameras import write_h36m_archives
+    rng = np.random.default_rng(31)
+    tree, camsp = str(tmp_path / "h36m.npz"), str(tmp_path / "cameras.npz")
+    write_h36m_archives(tree, camsp, rng, ["Walking", "Directions"], frames=400, sh=use_sh)
+    np.random.seed(5)
+    args = ["--epochs", "1", "--linear_size", "128", "--num_layers", "1", "--residual", "--batch_norm",
+            "--dropout", "0.5", "--learning_rate", "1e-3", "--camera_frame", "--action", "Walking",
+            "--data_dir", tree, "--cameras_path", camsp, "--train_dir", str(tmp_path / "exp")]
+    flags = predict_3dpose.build_parser().parse_args(args + (["--use_sh"] if use_sh else []))
+    d = predict_3dpose.load_data(flags)
+    n2 = sum(len(v) for v in d["train_set_2d"].values())
+    assert n2 == sum(len(v) for v in d["train_set_3d"].values())   # camera frame: one 3D row per 2D row
+    assert all(v.shape[1] == 32 for v in d["train_set_2d"].values())
+    assert all(v.shape[1] == 48 for v in d["train_set_3d"].values())
+    model = predict_3dpose.train(flags)
+    step = model.get_step()[0]
+    w = model.get_weights()
+    model.close()
+    assert step == n2 // 64                          # get_all_batches drops the n % 64 tail
+    assert all(np.isfinite(v).all() for v in w.values())
+    ck = predict_3dpose.train_dir_for(flags)
+    assert os.path.isfile(os.path.join(ck, "checkpoint-%d.index" % step))
