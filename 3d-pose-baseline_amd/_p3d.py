@@ -72,6 +72,7 @@ SIGNATURES = [
     ("p3d_train_fwd_bwd_lr", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
                                        c_float, c_float, c_float, c_void_p, c_void_p]),
     ("p3d_adam_apply", c_int32, [c_void_p, c_void_p]),
+    ("p3d_adam_apply_bucket", c_int32, [c_void_p, c_int32, c_void_p]),
     ("p3d_layer_grad_range", c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     ("p3d_stream_wait_grad", c_int32, [c_void_p, c_int32, c_void_p]),
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),

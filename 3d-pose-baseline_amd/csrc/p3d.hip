@@ -1499,6 +1499,10 @@ struct p3d_model {
   int serve_ks = 4;         // k_serve K slices per unit (env P3D_SERVE_KS: 8 or 4)
   int serve_split = 2;      // k_serve5 groups per XCD (env P3D_SERVE_SPLIT: 1, 2 or 4)
   std::vector<hipEvent_t> gev;   // per-bucket gradient-ready events (p3d_grad_buckets / p3d_grad_events)
+  std::vector<hipEvent_t> aev;   // per-bucket "parameters free" events: the backward's last reader of the
+                                 // bucket's parameters (dgrad of its lowest layer) has been issued
+  std::vector<AdamTable> bat;    // per-bucket optimizer tables (p3d_adam_apply_bucket)
+  std::vector<int> bat_blocks;
   std::vector<int> bucket_lo;    // lowest layer of each bucket, buckets in backward order (layers hi..lo)
   const AdamFuse* alpha_af = nullptr;  // set during p3d_train_fwd_bwd_lr: the backward forms the step's alpha
   AdamFuse dp_af{};              // hyper-parameters of the last p3d_train_fwd_bwd_lr (p3d_adam_apply)
@@ -1595,6 +1599,7 @@ bool g_exit_hooked = false;
 void release_model(p3d_model* m) {
   (void)hipDeviceSynchronize();
   for (hipEvent_t e : m->gev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : m->aev) (void)hipEventDestroy(e);
   free_all(m);
   delete m;
 }
@@ -2840,8 +2845,12 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     side_used = true;
     return P3D_OK;
   };
+  // bucket kb's parameters are free for its optimizer once dgrad of its lowest layer (the last
+  // reader of W / Wd of the bucket) is issued: its event at the top of the next iteration
+  int aev_pending = -1;
   auto flush_bucket = [&](int l) -> int {   // bucket kb ends at layer l: its tiles, then its event
     if (!bucketed || kb >= m->bucket_lo.size() || l != m->bucket_lo[kb]) return P3D_OK;
+    aev_pending = (int)kb;
     if (mw.n > 0) {
       ProfScope ps(m, "wgrad_bucket");
       go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
@@ -2866,6 +2875,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     return P3D_OK;
   };
   for (int l = nl - 1; l >= 0; --l) {
+    if (aev_pending >= 0) { HIP_TRY(hipEventRecord(m->aev[aev_pending], st)); aev_pending = -1; }
     const Layer& ly = m->layers[l];
     WgradArgs wa{};
     wa.X = (l == 0) ? m->x_cached : m->act[l - 1]; wa.ldx = c.input_size; wa.xpk = (l != 0);
@@ -2994,6 +3004,9 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   }
   if (!m->gev.empty() && !bucketed && !c.max_norm)   // (per-layer k_wgrad form: every bucket at the end)
     for (hipEvent_t e : m->gev) HIP_TRY(hipEventRecord(e, st));
+  if (aev_pending >= 0) { HIP_TRY(hipEventRecord(m->aev[aev_pending], st)); aev_pending = -1; }
+  if (!bucketed)
+    for (hipEvent_t e : m->aev) HIP_TRY(hipEventRecord(e, st));
   if (side_used) {   // join: the caller's stream (and a graph being captured on it) waits for the side
     HIP_TRY(hipEventRecord(m->sev[nl], m->side));
     HIP_TRY(hipStreamWaitEvent(st, m->sev[nl], 0));
@@ -3014,15 +3027,47 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
 extern "C" int p3d_grad_buckets(p3d_model* m, int32_t n, const int32_t* lowest) {
   if (!m) return fail(P3D_ERR_ARG, "p3d_grad_buckets: null model");
   const int nl = (int)m->layers.size();
+  if (n > P3D_MAX_W) return fail(P3D_ERR_ARG, "p3d_grad_buckets: bad bucket count");
   if (n < 0 || n > nl || (n > 0 && !lowest)) return fail(P3D_ERR_ARG, "p3d_grad_buckets: bad bucket count");
   for (int k = 0; k < n; ++k)   // contiguous, backward order, the last one ending at layer 0
     if (lowest[k] < 0 || lowest[k] >= nl || (k > 0 && lowest[k] >= lowest[k - 1]) || (k == n - 1 && lowest[k] != 0))
       return fail(P3D_ERR_ARG, "p3d_grad_buckets: lowest layers must decrease and end at layer 0");
   for (hipEvent_t e : m->gev) HIP_TRY(hipEventDestroy(e));
+  for (hipEvent_t e : m->aev) HIP_TRY(hipEventDestroy(e));
   m->gev.clear();
+  m->aev.clear();
+  m->bat.clear();
+  m->bat_blocks.clear();
   m->bucket_lo.assign(lowest, lowest + n);
   m->gev.resize((size_t)n, nullptr);
+  m->aev.resize((size_t)n, nullptr);
   for (hipEvent_t& e : m->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t& e : m->aev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // per-bucket optimizer tables: the weight tiles of the bucket's layers and the 1-D tensors
+  // (biases, gamma, beta) inside their flat ranges -- the whole-model table split by bucket
+  for (int k = 0; k < n; ++k) {
+    const int hi = k == 0 ? nl - 1 : lowest[k - 1] - 1, lo = lowest[k];
+    const int64_t fb = m->layers[lo].w, fe = hi + 1 < nl ? m->layers[hi + 1].w : m->n_flat;
+    AdamTable t{};
+    int tiles = 0, vch = 0;
+    for (int wi = 0; wi < m->at.nw; ++wi) {
+      if (m->at.off[wi] < fb || m->at.off[wi] >= fe) continue;
+      const int j = t.nw++;
+      t.K[j] = m->at.K[wi]; t.N[j] = m->at.N[wi]; t.off[j] = m->at.off[wi]; t.wf[j] = m->at.wf[wi]; t.wd[j] = m->at.wd[wi];
+      t.tile_begin[j] = tiles;
+      tiles += m->at.tile_begin[wi + 1] - m->at.tile_begin[wi];
+    }
+    t.tile_begin[t.nw] = tiles;
+    for (int vi = 0; vi < m->at.nv; ++vi) {
+      if (m->at.voff[vi] < fb || m->at.voff[vi] >= fe) continue;
+      const int j = t.nv++;
+      t.voff[j] = m->at.voff[vi]; t.vlen[j] = m->at.vlen[vi]; t.vbegin[j] = vch;
+      vch += m->at.vbegin[vi + 1] - m->at.vbegin[vi];
+    }
+    t.vbegin[t.nv] = vch;
+    m->bat.push_back(t);
+    m->bat_blocks.push_back(tiles + vch);
+  }
   return P3D_OK;
 }
 
@@ -3102,6 +3147,45 @@ extern "C" int p3d_adam_apply(p3d_model* m, void* stream) {
     return adam_launch(m, -1.0f, m->dp_af.lr0, m->dp_af.decay_steps, m->dp_af.decay_rate, (hipStream_t)stream);
   m->alpha_ready = false;
   return adam_launch(m, -2.0f, m->dp_af.lr0, m->dp_af.decay_steps, m->dp_af.decay_rate, (hipStream_t)stream);
+}
+
+// The optimizer of ONE gradient bucket (p3d_grad_buckets), for the caller's stream right after
+// that bucket's all-reduce: the stream first waits until the backward has issued the last
+// reader of the bucket's parameters (dgrad of its lowest layer), then TF1 Adam + re-pack of
+// the bucket's tensors with the alpha the backward formed; the last bucket's launch advances
+// the step state.  Per element the arithmetic of p3d_adam_apply (bit-identical results); the
+// buckets' optimizers overlap the rest of the backward instead of following it.  Without a
+// backward-formed alpha (P3D_TRAIN_SPLIT=0) the last bucket runs p3d_adam_apply's fallback and
+// the others nothing.
+extern "C" int p3d_adam_apply_bucket(p3d_model* m, int32_t bucket, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_adam_apply_bucket: null model");
+  if (m->bat.empty()) return fail(P3D_ERR_STATE, "p3d_adam_apply_bucket: no gradient buckets (p3d_grad_buckets)");
+  if (bucket < 0 || bucket >= (int32_t)m->bat.size()) return fail(P3D_ERR_ARG, "p3d_adam_apply_bucket: bad bucket");
+  if (m->dp_af.decay_steps <= 0.f) return fail(P3D_ERR_STATE, "p3d_adam_apply_bucket: no p3d_train_fwd_bwd_lr before it");
+  if (m->cfg.max_norm) return fail(P3D_ERR_STATE, "p3d_adam_apply_bucket: max_norm models take p3d_adam_apply");
+  hipStream_t st = (hipStream_t)stream;
+  const bool last = bucket == (int32_t)m->bat.size() - 1;
+  HIP_TRY(hipStreamWaitEvent(st, m->aev[bucket], 0));
+  if (!m->alpha_ready) {
+    if (!last) return P3D_OK;
+    return adam_launch(m, -1.0f, m->dp_af.lr0, m->dp_af.decay_steps, m->dp_af.decay_rate, st);
+  }
+  m->serve_ec_dirty = true;
+  AdamArgs a{};
+  a.w = m->flat[0]; a.g = m->flat[1]; a.m = m->flat[2]; a.v = m->flat[3];
+  a.wpk = m->wpk; a.st = m->dstate;
+  a.lr_host = -2.0f; a.lr0 = m->dp_af.lr0; a.decay_steps = m->dp_af.decay_steps; a.decay_rate = m->dp_af.decay_rate;
+  a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
+  a.wblocks = m->bat[bucket].tile_begin[m->bat[bucket].nw];
+  a.alpha_dev = m->alpha_dev;
+  a.advance = last ? m->dstate : nullptr;
+  if (m->bat_blocks[bucket] > 0) {
+    ProfScope ps(m, "adam_bucket");
+    go(ps, k_adam_pack, dim3(m->bat_blocks[bucket]), dim3(256), st, a, m->bat[bucket]);
+    LAUNCH_CHECK("k_adam_pack (bucket)");
+  }
+  if (last) m->alpha_ready = false;
+  return P3D_OK;
 }
 
 // One whole single-GPU TF1 training step (session.run([updates, loss, ...]),

@@ -60,12 +60,8 @@
 #define P3D_SERVE_FLAG0 256
 #define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 64)   // flags of up to 64 groups (k_serve6 S <= 8)
 // the model's serve sync allocation: k_serve6 banks 0 / 1 (group flags), the k_serve5 bank, then
-// k_serve6's device epoch word (bank = epoch & 1) on a line of its own, its census counters C[x]
-// (arrivals on XCD x over all launches, never reset) and their bases B[x] (C[x] at the end of the
-// previous launch's census), each on a 128-B line of its own
-#define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 32 + 512)
-#define P3D_SERVE_CENSUS_C 32          // word offsets from the epoch word
-#define P3D_SERVE_CENSUS_B (32 + 256)
+// k_serve6's device epoch word (bank = epoch & 1) on a line of its own
+#define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 64)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
@@ -118,7 +114,7 @@ struct ServeArgs {
   int* err;            // host-visible (pinned) error word: 1 = a bounded spin ran out, 2 = a placement
                        // the launch was not sized for
   unsigned* epoch;     // k_serve6: launches so far (device-side, advanced by the launch itself)
-  int census_extra;    // test hook: the census waits for this many workgroups beyond the grid
+  int census_extra;    // test hook: k_serve5's census waits for this many workgroups beyond the grid; k_serve6 takes it as a placement failure
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)
   const float* ecg;    // k_serve6: epilogue constants per layer and 16-column tile (k_serve_prep)

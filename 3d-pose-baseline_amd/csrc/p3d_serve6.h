@@ -13,11 +13,12 @@
 //
 // One launch per call: the sync words alternate between two banks picked on the device (the
 // launch reads an epoch word, uses bank epoch & 1, zeroes the other for the next launch, and one
-// workgroup advances the epoch once every workgroup has read it: the census guarantees that),
+// workgroup advances the epoch at the end of its work, long after every workgroup read it),
 // so a launch needs no memset in front and captured graphs replay correctly.  The epilogue
 // constants come from a table k_serve_prep forms per parameter version.
 //
-// What differs from k_serve5 (everything else -- census by hardware XCD id, flag hand-offs in
+// What differs from k_serve5 (everything else -- XCD-local groups (k_serve6: placed by the
+// dispatcher's round-robin, checked against the hardware XCD id), flag hand-offs in
 // the XCD's L2, sc1 reads of other CUs' data, 4-wave K-split contraction with a register ring,
 // epilogue constants in LDS, steps pipelined when a group has several -- is the same design):
 //   * work is dealt in 16-column tiles, not 32-column units: member r of a group of n owns the
@@ -34,7 +35,7 @@
 
 // Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
 // rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
-// [0] start, [1] census, [2] input layer, [3] first hand-off; per hidden phase ph at 8 ph:
+// [0] start, [1] placement, [2] input layer, [3] first hand-off; per hidden phase ph at 8 ph:
 // [0] begin, [1] contraction, [2] K-combine, [3] epilogue, [4] hand-off; at 8 (NH + 1): [0]
 // the output reduction.  wall_clock64 (100 MHz).
 #ifdef P3D_TRACE
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ float ecm[P3D_SERVE_MAXL];
   __shared__ int sh[32];
   // wave-uniform values the compiler cannot prove uniform (the wave index, everything read
-  // from the census in LDS) go through readfirstlane: they end in scalar registers, and
+  // from LDS) go through readfirstlane: they end in scalar registers, and
   // buffer loads with a scalar offset need no per-lane waterfall loop
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
@@ -121,52 +122,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   unsigned long long* tr6 = nullptr;
 #endif
 
-  // ---- census: XCD id, rank within the XCD, wait for every workgroup ---------------------
-  // The sync words come in two banks used by alternate launches, picked by the device epoch
+  // ---- placement: XCD id, rank within the XCD ---------------------------------------------
+  // The dispatcher deals a launch's workgroups to the 8 XCDs round-robin (consecutive
+  // workgroups on consecutive XCDs, from a starting XCD that varies between launches): with
+  // grid % 8 == 0 every XCD holds grid / 8 of them, workgroup b being member b / 8 of the XCD
+  // its hardware XCC id names -- the placement needs no census.  A grid the host did not size
+  // (grid % 8 != 0) or an S out of range sets the error word and fills the output with NaN; a
+  // dispatch that broke the pattern leaves some member of a group missing, and a workgroup that
+  // is not resident (CUs held by other work) is missing too: the group's bounded hand-off waits
+  // (group_sync) find either, and report and poison instead of hanging.  (Round 2's census -- a
+  // counter per XCD and a wait for every arrival -- cost ~3-4 us of memory-side round trips at
+  // the start of every launch.)
+  // The flag words come in two banks used by alternate launches, picked by the device epoch
   // word: this launch zeroes the other bank for the next one (stream order: the launch that
-  // used it has completed), so a launch needs no memset in front of it
-  // Arrival in ONE memory round trip: the epoch read, the returning add on this XCD's census
-  // counter C[x] and the reads of the launch's census bases B[0..7] are in flight together (the
-  // counters are never reset: this launch's rank on XCD x is the add's old value - B[x], its
-  // count there C[x] - B[x]).  Were the counters in the epoch's bank, the arrival would wait for
-  // the epoch first: two dependent round trips to the memory side (~1 us each) before the wait.
-  unsigned* const censc = p.epoch + P3D_SERVE_CENSUS_C;
-  unsigned* const censb = p.epoch + P3D_SERVE_CENSUS_B;
+  // used it has completed), so a launch needs no memset in front of it.
+  const int nxg = (int)(gridDim.x >> 3);
+  unsigned xr;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+  const int xcc = (int)(xr & 7u), rx = (int)(blockIdx.x >> 3);
+  unsigned ep = 0;
   if (tid == 0) {
-    unsigned xr;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
-    const int xc = (int)(xr & 7u);
-    const unsigned ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned old = __hip_atomic_fetch_add(censc + 32 * xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned bs[8];
-#pragma unroll
-    for (int x = 0; x < 8; ++x) bs[x] = __hip_atomic_load(censb + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh[0] = xc;
-    sh[1] = (int)(old - bs[xc]);
-    sh[3] = (int)(ep & 1u);
+    ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (in flight)
+    const bool bad = (gridDim.x & 7u) != 0u || S < 1 || S > 8 || p.census_extra;
+    sh[0] = (int)(((unsigned)xcc - blockIdx.x) & 7u);   // (trace: the launch's starting XCD)
+    sh[2] = bad ? 1 : 0;
     sh[4] = 0;                               // some wave of this workgroup is broken (group_sync)
-#pragma unroll
-    for (int x = 0; x < 8; ++x) sh[24 + x] = (int)bs[x];
+    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __syncthreads();
-#ifdef P3D_TRACE
-  if (tid == 0 && blockIdx.x < 1024) {     // per workgroup: start, arrival, census end, XCD | rank
-    g_p3d_trace[16384 + blockIdx.x * 4 + 0] = t_start;
-    g_p3d_trace[16384 + blockIdx.x * 4 + 1] = wall_clock64();
-    g_p3d_trace[16384 + blockIdx.x * 4 + 3] = (unsigned long long)(sh[0] | (sh[1] << 8));
-  }
-#endif
-  const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
-  unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
-  {
-    unsigned* other = p.sync + (bank ^ 1) * P3D_SERVE_SYNC_WORDS;
-    for (int i = blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
-  }
-  // After its arrival (XCD id, rank) a workgroup guesses its place assuming every XCD holds
-  // grid / 8 workgroups (the dispatcher's round-robin) and requests its first input-layer
-  // operands and epilogue constants; the wait for every workgroup's arrival then hides their
-  // latency.  The guess is used only if the final counts confirm it (every workgroup sees the
-  // same counts, so all decide alike); otherwise the loads are re-issued.
   const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
   constexpr int ECN = ((P3D_SERVE_MAXL - 1) * ECT * 48 + 255) / 256;
   // place of this workgroup for XCD counts cnt(x): member r of group gid (gi-th of ng groups
@@ -220,67 +202,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     wq = tid < nl_ec ? p.ecg[(int64_t)nl_ec * T * 48 + tid] : 1.f;
   };
-  const int xcc = __builtin_amdgcn_readfirstlane(sh[0]), rx = __builtin_amdgcn_readfirstlane(sh[1]);
-  const int nxg = (int)gridDim.x / 8;
-  const bool guessable = (gridDim.x % 8) == 0 && S >= 1 && S <= 8;
-  int g_r = 0, g_n = 1, g_gid = 0, g_gi = -1, g_ng = 0;
-  if (guessable) {
-    place([&](int) { return nxg; }, xcc, rx, g_r, g_n, g_gid, g_gi, g_ng);
-    prefetch(g_gi, (T * g_r) / g_n, (T * (g_r + 1)) / g_n);
-  }
-  if (tid == 0) {   // the wait: every workgroup arrived (this launch's counts C[x] - B[x] sum to the grid)
-    const int maxn = (S < 1 || S > 8) ? -1 : 64 * S;
-    int bad = 0, spin = 0;
-    unsigned c[8];
-    const unsigned expect = gridDim.x + (unsigned)p.census_extra;
-    while (true) {
-      unsigned tot = 0;
-#pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        c[x] = __hip_atomic_load(censc + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)sh[24 + x];
-        tot += c[x];
-      }
-      if (tot >= expect) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spin > P3D_SERVE_SPIN) { bad = 1; break; }
-    }
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      sh[8 + x] = (int)c[x];
-      if ((int)c[x] > maxn) bad = 1;   // judged on every XCD's count: all workgroups decide alike
-    }
-    if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    sh[2] = bad;
-  }
+  int r, n, gid, gi, ng;
+  place([&](int) { return nxg; }, xcc, rx, r, n, gid, gi, ng);
+  // the first unit's input-layer operands and the epilogue constants in flight with the epoch read
+  prefetch(gi, (T * r) / n, (T * (r + 1)) / n);
+  if (tid == 0) sh[3] = (int)(ep & 1u);
   __syncthreads();
 #ifdef P3D_TRACE
-  if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[16384 + blockIdx.x * 4 + 2] = wall_clock64();
+  if (tid == 0 && blockIdx.x < 1024) {     // per workgroup: start, placement known, XCD | rank
+    g_p3d_trace[16384 + blockIdx.x * 4 + 0] = t_start;
+    g_p3d_trace[16384 + blockIdx.x * 4 + 1] = wall_clock64();
+    g_p3d_trace[16384 + blockIdx.x * 4 + 2] = wall_clock64();
+    g_p3d_trace[16384 + blockIdx.x * 4 + 3] = (unsigned long long)(xcc | (rx << 8) | (sh[0] << 16));
+  }
 #endif
+  const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
+  unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
+  {
+    unsigned* other = p.sync + (bank ^ 1) * P3D_SERVE_SYNC_WORDS;
+    for (int i = P3D_SERVE_FLAG0 + blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
+  }
   if (sh[2]) {
-    // the census failed (not every workgroup resident within the bounded wait): no row of this
-    // launch is computed; each workgroup fills a stripe of the output with NaN, so a caller who
-    // skips p3d_serve_check / p3d_error_flags still never reads a stale or unwritten row as a
-    // result (the error word is set)
+    // a placement this launch cannot use: no row of it is computed by this workgroup; it fills
+    // a stripe of the output with NaN, so a caller who skips p3d_serve_check / p3d_error_flags
+    // never reads a stale or unwritten row as a result (the error word is set)
     const float qnan = __builtin_nanf("");
     for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < p.M * p.ND; e += (int64_t)gridDim.x * 256) p.y[e] = qnan;
   } else {
-  // One workgroup -- rank 0 of the lowest-numbered XCD that holds workgroups (all see the same
-  // counts) -- advances the epoch and moves the bases to the final counters for the next launch,
-  // at the END of its work: the epoch and base reads of the others were issued together with
-  // their arrivals (not ahead of them), so an update right after the census could overtake a read
-  // still in flight; a launch's length later every read has long returned (a wave's memory
-  // requests complete in bounded time -- a context-saved wave drains them first).
-  bool leader = false;
-  if (tid == 0 && sh[1] == 0) {
-    int lead = 0;
-    while (lead < 7 && sh[8 + lead] == 0) ++lead;
-    leader = sh[0] == lead;
-  }
-  bool guess_held = guessable;
-#pragma unroll
-  for (int x = 0; x < 8; ++x) guess_held = guess_held && __builtin_amdgcn_readfirstlane(sh[8 + x]) == nxg;
-  int r, n, gid, gi, ng;
-  place([&](int x) { return __builtin_amdgcn_readfirstlane(sh[8 + x]); }, xcc, rx, r, n, gid, gi, ng);
+  // workgroup 0 advances the epoch for the next launch at the END of its work (every other
+  // workgroup read it at its start, a launch's length earlier; a late one belongs to a group
+  // whose hand-offs time out and report)
+  const bool leader = tid == 0 && blockIdx.x == 0;
   if (gi < 0) {                              // a placement the host did not size this form for:
     if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     gi = p.nb;                               // the whole group reports instead of computing
@@ -328,8 +280,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
     }
   };
-  // the guess failed: the first unit's operands and the constants again, for the real place
-  if (!guess_held) prefetch(gi, t_lo, t_hi);
   {   // epilogue constants of this member's tiles -- bias, inv = gamma / sqrt(var + eps),
       // shift = beta - mean * inv (the arithmetic of every other path), each layer's max-norm
       // divisor -- copied from the table k_serve_prep forms once per parameter version
@@ -684,12 +634,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
   }
-  if (leader) {
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-      __hip_atomic_store(censb + 32 * x, (unsigned)sh[24 + x] + (unsigned)sh[8 + x], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (leader) __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

@@ -77,7 +77,7 @@ def plan_buckets(ranges, min_elems):
     return [tuple(b) for b in out]
 
 
-def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
+def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream, after=None):
     """Bucketed DP gradient average that overlaps the backward.
 
     For each bucket k (backward order), ``comm_stream`` waits for its gradient-ready event
@@ -87,7 +87,9 @@ def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
     the result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).  Under gloo (tests:
     several ranks on one GPU) each bucket is copied to the host on ``comm_stream`` after
     its event -- the same event ordering, host-staged: a bucket read before its layer's
-    gradients are final would differ from the single all-reduce.
+    gradients are final would differ from the single all-reduce.  ``after(k, stream_handle)``
+    (optional) is issued on ``comm_stream`` behind bucket k's reduced slice -- the bucket's
+    optimizer (p3d_adam_apply_bucket) -- and the current stream then waits for ``comm_stream``.
     """
     import torch
     import torch.distributed as dist
@@ -100,13 +102,24 @@ def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream):
                 dist.all_reduce(h, op=dist.ReduceOp.SUM)
                 h.div_(world)
                 t[lo:hi].copy_(h)
+                if after is not None:
+                    after(k, comm_stream.cuda_stream)
         torch.cuda.current_stream().wait_stream(comm_stream)
         return t
     works = []
     with torch.cuda.stream(comm_stream):
         for k, (lo, hi, _) in enumerate(buckets):
             wait_ready(k, comm_stream.cuda_stream)
-            works.append(dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG, async_op=True))
+            if after is None:
+                works.append(dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG, async_op=True))
+            else:
+                # a synchronous collective runs on the current stream (comm_stream) itself: the
+                # bucket's optimizer queues right behind it.  (An async one plus work.wait() from
+                # comm_stream crashed HIP graph capture at capture end.)
+                dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG)
+                after(k, comm_stream.cuda_stream)
+    if after is not None:
+        torch.cuda.current_stream().wait_stream(comm_stream)
     for w in works:
         w.wait()
     return t

@@ -554,8 +554,11 @@ class LinearModel(object):
             check(lib().p3d_train_fwd_bwd_lr(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
                                              self.rank * B, self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
                   "p3d_train_fwd_bwd_lr")
-            self._allreduce_grads()
-            check(lib().p3d_adam_apply(self._h, self.stream()), "p3d_adam_apply")
+            if self._buckets and self._bucket_adam and not self.max_norm:
+                self._allreduce_grads(bucket_adam=True)   # each bucket's Adam behind its all-reduce
+            else:
+                self._allreduce_grads()
+                check(lib().p3d_adam_apply(self._h, self.stream()), "p3d_adam_apply")
         self._step_host += 1
         return loss_t, y
 
@@ -584,6 +587,9 @@ class LinearModel(object):
         import torch.distributed as dist
         if bucket_mb is None:
             bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "8"))
+        # each bucket's optimizer right behind its all-reduce (p3d_adam_apply_bucket), overlapping
+        # the rest of the backward; P3D_DP_BUCKET_ADAM=0: one p3d_adam_apply after the last bucket
+        self._bucket_adam = os.environ.get("P3D_DP_BUCKET_ADAM", "1") != "0"
         on = (bucket_mb > 0 and self.data_parallel and dist.is_initialized()
               and (dist.get_backend() == "nccl" or gloo))
         self._buckets = None
@@ -601,11 +607,15 @@ class LinearModel(object):
             check(lib().p3d_grad_buckets(self._h, 0, None), "p3d_grad_buckets")
         return self._buckets
 
-    def _allreduce_grads(self):
+    def _allreduce_grads(self, bucket_adam=False):
         if getattr(self, "_buckets", None):
             def wait(k, handle):
                 check(lib().p3d_stream_wait_grad(self._h, k, handle), "p3d_stream_wait_grad")
-            dist_utils.allreduce_mean_buckets_(self.flat["grads"], self._buckets, wait, self._comm)
+
+            def adam(k, handle):
+                check(lib().p3d_adam_apply_bucket(self._h, k, handle), "p3d_adam_apply_bucket")
+            dist_utils.allreduce_mean_buckets_(self.flat["grads"], self._buckets, wait, self._comm,
+                                               after=adam if bucket_adam else None)
         else:
             dist_utils.allreduce_mean_(self.flat["grads"])
 

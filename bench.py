@@ -624,7 +624,17 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None, dp=N
     # p, m, v read+write, g read (7 x 4 B) + Wf, Wd written (2 x 4 B per weight element)
     n_params = sum(n for _, n, k, _ in model.param_table if k == 0)
     n_w = sum(n for nm, n, k, _ in model.param_table if k == 0 and nm.split("/")[-1][0] == "w")
-    if "adam_pack" in prof:   # data parallel: separate optimizer pass after the all-reduce
+    if "adam_bucket" in prof:   # data parallel: each bucket's optimizer behind its all-reduce
+        cnt, avg_us, _, _ = prof["adam_bucket"]
+        nb = len(model._buckets or ()) or 1
+        byts = 7 * 4 * n_params + 2 * 4 * n_w       # the whole model's, over the step's nb launches
+        achieved = byts / (nb * avg_us * 1e-6) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_adam_pack per gradient bucket (TF1 Adam + Wf/Wd re-pack, on the comm stream behind "
+                          "the bucket's all-reduce, overlapping the rest of the backward), %d per step" % nb,
+                "bytes_per_step": byts, "avg_us": round(avg_us, 3), "launches_timed": cnt}
+    elif "adam_pack" in prof:   # data parallel: separate optimizer pass after the all-reduce
         cnt, avg_us, _, _ = prof["adam_pack"]
         byts = 7 * 4 * n_params + 2 * 4 * n_w
         achieved = byts / (avg_us * 1e-6) / 1e9

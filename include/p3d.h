@@ -196,6 +196,15 @@ int p3d_train_fwd_bwd_lr(p3d_model* m, const float* x, const float* t, int64_t B
                          float* loss_dev, void* stream);
 int p3d_adam_apply(p3d_model* m, void* stream);
 
+/* p3d_adam_apply split by gradient bucket (p3d_grad_buckets), each part issued on the stream of
+ * that bucket's all-reduce right after it: the stream waits until the last backward has issued
+ * the last reader of the bucket's parameters (the data-gradient launch of its lowest layer),
+ * then Adam + re-pack of the bucket's tensors; the last bucket's launch advances the step
+ * state.  Every bucket exactly once per step, in bucket order on one stream; bit-identical
+ * to p3d_adam_apply.  The optimizer then overlaps the rest of the backward.  max_norm models:
+ * P3D_ERR_STATE (they take p3d_adam_apply). */
+int p3d_adam_apply_bucket(p3d_model* m, int32_t bucket, void* stream);
+
 /* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
  * the TF1 Adam update, global_step += 1.  By default (env P3D_FUSE_ADAM=1 at p3d_create) the
  * update runs inside the batched weight-gradient launch (k_wgrad_multi: no separate optimizer

@@ -73,7 +73,8 @@ def main():
         print(json.dumps({"workgroups": len(wg), "start_q": q(st), "arrive_q": q(ar), "census_end_q": q(ce),
                           "arrive_minus_start_q": q((wg[:, 1] - wg[:, 0]) / 100.0),
                           "per_xcd_last_start": [round(float(((wg[(wg[:, 3] & 255) == x, 0] - t0) / 100.0).max()), 2)
-                                                 if ((wg[:, 3] & 255) == x).any() else None for x in range(8)]}))
+                                                 if ((wg[:, 3] & 255) == x).any() else None for x in range(8)],
+                          "start_xcd_offsets": sorted(set(int(v) for v in ((wg[:, 3] >> 16) & 255)))}))
 
 
 if __name__ == "__main__":
