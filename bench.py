@@ -1049,7 +1049,7 @@ def cpu_data_baseline(seconds):
             "sample": "%d camera-poses (4 sequences x 2600 frames x 4 cameras per pass), %.1f s" % (done, dt)}
 
 
-def main():
+def build_arg_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -1083,6 +1083,11 @@ def main():
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="print the N-rank launch command --gpus N > 1 would run, and exit")
+    return ap
+
+
+def main():
+    ap = build_arg_parser()
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: start N fresh ranks and wait for them.  This process touches
@@ -1132,8 +1137,8 @@ def main():
                     dv, ddt, droof, dmode = bench_train(args, rank, world, steps=args.train_steps, warmup=64, dp=True)
                     train["dp_form_1rank"] = {
                         "workload": "the data-parallel step (fwd + bwd with %g MB gradient buckets, one weight-gradient "
-                                    "launch each, RCCL all-reduce(AVG) on a 1-rank group, TF1 Adam + re-pack + step "
-                                    "advance in one launch)" % args.dp_bucket_mb,
+                                    "launch each, RCCL all-reduce(AVG) on a 1-rank group, each bucket's TF1 Adam + "
+                                    "re-pack behind its all-reduce, step advance in the last)" % args.dp_bucket_mb,
                         "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
                         "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
                         "event_pair_avg_us": droof.get("event_pair_avg_us")}
