@@ -377,27 +377,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the four slices in slice order (after the caller's __syncthreads)
   // the same sums with every partial requested before the first add (16 tiles per slice in
   // flight: the launch's last reduction, nothing else is live then)
+  // every load of a 16-tile chunk, for all RE elements, issued before the first add (clamped
+  // addresses, no branch around a load: one round of L2 latency per chunk, not one per element)
   auto red_slices_all = [&](const float* pb) {
     const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(pb);
     const int tb = (T * w) >> 2, te = (T * (w + 1)) >> 2;
+    f32x4 ss[RE];
+#pragma unroll
+    for (int j = 0; j < RE; ++j) ss[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t0 = tb; t0 < te; t0 += 16) {
+      f32x4 v[RE][16];
+#pragma unroll
+      for (int j = 0; j < RE; ++j) {
+        const int el = lane + 64 * j, elc = el < ecnt ? el : 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[j][k] = p3d_ld_sc1(rp, (min(t0 + k, te - 1) * E4 + es + elc) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < RE; ++j) {
+        ss[j] = t0 == tb ? v[j][0] : ss[j] + v[j][0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+          if (t0 + k < te) ss[j] += v[j][k];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < RE; ++j) {
       const int el = lane + 64 * j;
-      f32x4 ss = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (el < ecnt && tb < te) {
-        for (int t0 = tb; t0 < te; t0 += 16) {
-          f32x4 v[16];
-#pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (t0 + k < te) v[k] = p3d_ld_sc1(rp, ((t0 + k) * E4 + es + el) * 16);
-          if (t0 == tb) ss = v[0];
-          else ss += v[0];
-#pragma unroll
-          for (int k = 1; k < 16; ++k)
-            if (t0 + k < te) ss += v[k];
-        }
-      }
-      rsum[w * 64 * RE + el] = ss;
+      rsum[w * 64 * RE + el] = el < ecnt ? ss[j] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   const float qnan = __builtin_nanf("");
@@ -583,6 +590,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int k = 1; k < 4; ++k) sacc[j] += red[((k * RT + rt) * NCM + cc) * 64 + lane];
         }
+        P3D_S6_STAMP(trs && first_c, 8 * ph + 5);
         if (wsq_any)
 #pragma unroll
           for (int j = 0; j < UMAX; ++j) maxnorm_div(ph, sacc[j]);
@@ -605,6 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
           }
         }
+        P3D_S6_STAMP(trs && first_c, 8 * ph + 6);
         // red / rsum are rewritten by this member's next contraction of the phase
         if (c0 + NCM < t_hi) __syncthreads();
       }

@@ -6,7 +6,8 @@
 
 For every XCD group of the last launch (its first step): rank-0 member and the first member
 holding the most column tiles; times in us from the earliest workgroup start (wall_clock64,
-100 MHz).  Columns per hidden phase: contraction, K-combine, epilogue, hand-off wait.
+100 MHz).  Columns per hidden phase: contraction, K-combine, epilogue, hand-off wait, then inside the
+epilogue: the K-slice sums (LDS), the epilogue math + stores.
 """
 import ctypes
 import json
@@ -49,9 +50,9 @@ def main():
             continue
         ph = []
         for p in range(1, NH + 1):
-            b, c, k, e, h = (row[8 * p + i] for i in range(5))
+            b, c, k, e, h, r5, r6 = (row[8 * p + i] for i in (0, 1, 2, 3, 4, 5, 6))
             ph.append([round((c - b) / 100, 2), round((k - c) / 100, 2), round((e - k) / 100, 2),
-                       round((h - e) / 100, 2)])
+                       round((h - e) / 100, 2), round((r5 - k) / 100, 2), round((r6 - r5) / 100, 2)])
         # core clock over the contractions: s_memtime cycles / wall_clock64 (100 MHz) ticks
         cyc = sum(row[64 + 8 * p + 1] - row[64 + 8 * p] for p in range(1, NH + 1))
         wall = sum(row[8 * p + 1] - row[8 * p] for p in range(1, NH + 1))
