@@ -315,7 +315,6 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     sq = p3d_colsum16(sq);
     if (p.bn == 4) {
       const int R = tgy;
-      float st[P3D_XCHG_MAXR], qt[P3D_XCHG_MAXR];
       if (WK > 1) p3d_xchg_post(&xpub, q == 0, i, sum, sq, xtag);
       else p3d_xchg_put(p.xs, p.N, tby, col, q == 0 && cok, sum, sq, xtag);
       // the dropout uniforms do not depend on the statistics: formed while the siblings arrive
@@ -323,8 +322,12 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
 #pragma unroll
         for (int s = 0; s < RS; ++s) p3d_uniform_rows4(p.seed, ctr, p.site, p.row_off + m0 + 16 * s + 4 * q, cc, uu_x[s]);
       }
-      p3d_xchg_get(p.xs, p.N, R, cc, xtag, st, qt, tby);
+      if (R <= 4) p3d_xchg_moments<4>(p.xs, p.N, R, cc, xtag, tby, p.M, xmean, xvar);   // (wave-uniform)
+      else p3d_xchg_moments<P3D_XCHG_MAXR>(p.xs, p.N, R, cc, xtag, tby, p.M, xmean, xvar);
       p3d_xchg_done(p.xs, ct, tby);
+#ifdef P3D_TRACE
+      if (trace && lane == 0 && ct + tgx * tby < 2048) g_p3d_trace[16384 + (ct + tgx * tby) * 8 + 6] = wall_clock64();
+#endif
 #ifdef P3D_TRACE
       if (trace && lane == 0 && p3d_trace_idx < 4096) {   // slot 7: the hardware XCD of this workgroup
         unsigned xr;
@@ -332,17 +335,6 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
         g_p3d_trace[p3d_trace_idx * 8 + 7] = xr & 7u;
       }
 #endif
-      float S = 0.f;
-#pragma unroll
-      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
-        if (t < R) S += st[t];
-      const float fm = (float)p.M;
-      xmean = S / fm;
-      float M2 = 0.f;
-#pragma unroll
-      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
-        if (t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, p.M - 16 * t), xmean);
-      xvar = M2 / fm;
     }
   }
   if (p.bn == 3) {
@@ -775,10 +767,11 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
     sgx = p3d_colsum16(sgx);
     if (p.xchg) {   // exchange form: the row-tile siblings swap {sum g, sum g xhat}
       const int R = gy;
-      float at[P3D_XCHG_MAXR], bt[P3D_XCHG_MAXR];
       if (WK > 1) p3d_xchg_post(&xpub, q == 0, i, sg, sgx, xtag);
       else p3d_xchg_put(p.xs, p.K, by, col, q == 0 && cok, sg, sgx, xtag);
-      p3d_xchg_get(p.xs, p.K, R, cc, xtag, at, bt, by);
+      float xsg, xsgx;
+      if (R <= 4) p3d_xchg_sums<4>(p.xs, p.K, R, cc, xtag, by, xsg, xsgx);   // (wave-uniform)
+      else p3d_xchg_sums<P3D_XCHG_MAXR>(p.xs, p.K, R, cc, xtag, by, xsg, xsgx);
       p3d_xchg_done(p.xs, bx, by);
       if (defer_draw && p.draw && cok)
 #pragma unroll
@@ -788,11 +781,8 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
             const int row = m0 + 16 * s + 4 * q + r;
             if (row < p.M) p.draw[p3d_pk(row, col, ngK)] = dv[s][r];
           }
-      sg = 0.f;
-      sgx = 0.f;
-#pragma unroll
-      for (int t = 0; t < P3D_XCHG_MAXR; ++t)
-        if (t < R) { sg += at[t]; sgx += bt[t]; }
+      sg = xsg;
+      sgx = xsgx;
       if (!cok) return;
       if (by == 0 && q == 0) { p.dgamma[col] = sgx; p.dbeta[col] = sg; }
       const float fmx = (float)p.M;

@@ -162,7 +162,7 @@ __device__ __forceinline__ void p3d_xchg_put(const XchgSite& x, int N, int rt, i
 // ~3 us per exchange at R = 4), a straight run waits once per sweep.
 template <int NR>
 __device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, int col, unsigned tag,
-                                               float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR], int trace_rt) {
+                                               float (&a)[NR], float (&b)[NR], int trace_rt) {
   const __amdgpu_buffer_rsrc_t rn = p3d_rsrc(x.near), rs = p3d_rsrc(x.slots);
 #ifdef P3D_TRACE
   const int tix = (col >> 4) + (N >> 4) * trace_rt;
@@ -210,10 +210,37 @@ __device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, 
 #endif
 }
 
-__device__ __forceinline__ void p3d_xchg_get(const XchgSite& x, int N, int R, int col, unsigned tag,
-                                             float (&a)[P3D_XCHG_MAXR], float (&b)[P3D_XCHG_MAXR], int trace_rt = 0) {
-  if (R <= 4) p3d_xchg_get_n<4>(x, N, R, col, tag, a, b, trace_rt);     // B <= 64 (wave-uniform branch)
-  else p3d_xchg_get_n<P3D_XCHG_MAXR>(x, N, R, col, tag, a, b, trace_rt);
+// The combination after the swap, over NR slots (NR = 4 for B <= 64: the combine loops then
+// run 4 iterations, not 16 guarded ones -- 16 guarded Chan terms, each with its divide, had
+// cost ~0.5 us per forward launch).  Forward: the batch mean / variance (Chan, row-tile order);
+// backward: sum g, sum g xhat (row-tile order).  Same association as the split kernels.
+template <int NR>
+__device__ __forceinline__ void p3d_xchg_moments(const XchgSite& x, int N, int R, int col, unsigned tag, int rt,
+                                                 int M, float& mean, float& var) {
+  float st[NR], qt[NR];
+  p3d_xchg_get_n<NR>(x, N, R, col, tag, st, qt, rt);
+  float S = 0.f;
+#pragma unroll
+  for (int t = 0; t < NR; ++t)
+    if (t < R) S += st[t];
+  const float fm = (float)M;
+  mean = S / fm;
+  float M2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < NR; ++t)
+    if (t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, M - 16 * t), mean);
+  var = M2 / fm;
+}
+template <int NR>
+__device__ __forceinline__ void p3d_xchg_sums(const XchgSite& x, int N, int R, int col, unsigned tag, int rt,
+                                              float& sa, float& sb) {
+  float at[NR], bt[NR];
+  p3d_xchg_get_n<NR>(x, N, R, col, tag, at, bt, rt);
+  sa = 0.f;
+  sb = 0.f;
+#pragma unroll
+  for (int t = 0; t < NR; ++t)
+    if (t < R) { sa += at[t]; sb += bt[t]; }
 }
 
 // Row tile 0 of column tile ct, after its swap: the tile's next launch gets a new tag.

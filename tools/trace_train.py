@@ -33,6 +33,7 @@ assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
 nwg = int(os.environ.get("P3D_TRACE_NWG", "256"))   # workgroups of the traced launch
 t = buf.reshape(4096, 8)[:nwg, :6].astype(np.int64)
 t0 = t[:, 0].min()
+t0f = t0
 names = ["start", "gemm(w0)", "reduced", "bn+xchg", "philox", "stored"]
 for k, n in enumerate(names):
     d = (t[:, k] - t0) * 10.0 / 1000.0
@@ -59,3 +60,6 @@ print("sweeps per get: med %d max %d; memory-side sweeps med %d max %d"
 pa = us(e[:, 2]).reshape(4, gx).max(0)         # the latest sibling's publish acked
 print("get done - latest sibling acked: med %.2f max %.2f us"
       % (np.median(us(e[:, 3]).reshape(4, gx) - pa), (us(e[:, 3]).reshape(4, gx) - pa).max()))
+for k, n in ((6, "fwd: moments done (w0)"),):   # (the forward's own time base)
+    d = (e[:, k] - t0f) * 10.0 / 1000.0
+    print("%-20s min %6.2f  med %6.2f  max %6.2f us" % (n, d.min(), np.median(d), d.max()))
