@@ -20,6 +20,8 @@ def main():
     v, dt, roof, mode = bench.bench_train(args, 0, 1, steps=steps, warmup=64, dp=False)
     print(json.dumps({"form": "fused single-GPU", "us_per_step": round(1e6 * dt / steps, 2), "mode": mode,
                       "ev": roof.get("event_pair_avg_us")}), flush=True)
+    if os.environ.get("FUSED_ONLY"):
+        return
     for mb in (8.0, 4.0, 2.0, 0.0):
         for badam in ("1", "0"):
             if mb == 0.0 and badam == "1":

@@ -3,6 +3,7 @@
 #   1. rocprofv3 --kernel-trace --stats of `python3 bench.py --gpus 1 --steps 20 --warmup 5`
 #   2. two separate PMC passes (FETCH_SIZE, WRITE_SIZE) of the serve path alone at 20 steps
 #      per launch (tools/pmc_traffic.py turns them into HBM bytes per launch)
+#   3. the same for the cfg3 training step (bench.py --mode train)
 # Every step under its own time limit; the script stops at the first failure.
 set -e
 OUT=${1:-gpurun_out/prof}
@@ -12,4 +13,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 SERVE="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-streams --no-eval --no-data --no-api --no-stress --train-steps 0 --no-cpu"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- $SERVE > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- $SERVE > "$OUT/write.json" 2> "$OUT/write.err"
+# 3. the cfg3 fused training step (single GPU), kernel stats + the same two PMC passes
+TRAIN="python3 bench.py --gpus 1 --mode train --steps 64 --warmup 16 --no-cpu"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train_trace" -o run -- $TRAIN > "$OUT/train_under_rocprof.json" 2> "$OUT/train_under_rocprof.err"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/train_fetch" -o run -- $TRAIN > "$OUT/train_fetch.json" 2> "$OUT/train_fetch.err"
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/train_write" -o run -- $TRAIN > "$OUT/train_write.json" 2> "$OUT/train_write.err"
 echo profile-done
