@@ -1469,6 +1469,7 @@ struct p3d_model {
   int fwd_t = 0;            // inference layers in the transposed-accumulator form (env P3D_FWD_T=1;
                             // bit-identical, +3% single-stream, -2% at 4 streams: 58 vs 52 VGPRs)
   int in_wk = 2, out_wk = 16; // input / output layer variants (env P3D_IN_WK, P3D_OUT_WK; 0 = infer_wk)
+  int out_train_wk = 8;       // training output layer (fused MSE) variant (env P3D_OUT_TRAIN_WK)
   int out_big = 0;            // output layer tiling at M >= big_m (env P3D_OUT_BIG; 0 = the B <= 64 one)
   int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
@@ -1785,6 +1786,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
   if (const char* ev = getenv("P3D_FWD_T")) m->fwd_t = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_OUT_TRAIN_WK")) m->out_train_wk = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_BIG")) m->out_big = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
@@ -2133,10 +2135,11 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
   ProfScope ps(m, tags[whole_batch ? 1 : 0][kind]);
   int wk = whole_batch ? m->train_wk : m->infer_wk;
   if (!whole_batch && kind == 0 && m->in_wk) wk = m->in_wk;
-  if (!whole_batch && kind == 2 && m->out_wk) wk = m->out_wk;
   // training output layer (fused MSE, 12 workgroups at B = 64): the 8-deep ring (all of a wave's
-  // K slice requested at once) -- 6.85 vs 7.8 us with the inference tiling (A/B on one box)
-  else if (!whole_batch && kind == 2 && a.tgt) wk = 8;
+  // K slice requested at once) -- 6.85 vs 7.8 us with the inference tiling (A/B on one box);
+  // env P3D_OUT_TRAIN_WK overrides
+  if (!whole_batch && kind == 2 && a.tgt) wk = m->out_train_wk;
+  else if (!whole_batch && kind == 2 && m->out_wk) wk = m->out_wk;
   const dim3 g16((a.N + 15) / 16, (a.M + 15) / 16);
   if (m->fwd_t && !whole_batch && (a.bn == 0 || a.bn == 1) && !a.z_save && !a.tgt && wk == (kind == 0 ? 2 : kind == 1 ? 82 : 16)) {
     // inference, transposed-accumulator form (float4 epilogue, 1 KB tile stores)
