@@ -970,7 +970,16 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
 }
 
 // dW tile (bx, by) = 64 columns x 64 rows of X^T dZ (and db from the by == 0 row of tiles)
+#ifdef P3D_TRACE   // k_wgrad_multi timeline (tools/trace_wgrad.py): per workgroup at 4096 + 8 b
+#define P3D_WG_STAMP(k)                                                                                 \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 1500) g_p3d_trace[4096 + blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define P3D_WG_STAMP(k) do { } while (0)
+#endif
 __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
+  P3D_WG_STAMP(0);
   __shared__ __attribute__((aligned(16))) float xs[64 * WG_LDS_STRIDE];
   __shared__ __attribute__((aligned(16))) float zs[64 * WG_LDS_STRIDE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -991,6 +1000,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     p3d_stage64_store(xs, sx, p.xpk);
     p3d_stage64_store(zs, sz, p.zpk);
     __syncthreads();
+    P3D_WG_STAMP(1);
 #pragma unroll 4
     for (int t = 0; t < 16; ++t) {
       const int m = 4 * t + q;
@@ -1008,6 +1018,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     }
     __syncthreads();
   }
+  P3D_WG_STAMP(2);
   float alpha = 0.f;
   if (p.adam)
     alpha = p.alpha_dev ? alpha_pre : p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
@@ -1047,6 +1058,10 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     __syncthreads();
     p3d_adam_tile64(tile, nullptr, p.woff, p.K, p.N, k0, n0, p.w, p.m, p.v, p.wd, p.wf, alpha,
                     1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps);
+#ifdef P3D_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    P3D_WG_STAMP(3);
     return;
   }
 #pragma unroll
