@@ -1099,6 +1099,7 @@ struct WgradMulti {
   WgradLayer ly[P3D_WG_MULTI];
 };
 __device__ __forceinline__ void p3d_wgrad_multi_tile(const WgradMulti& mw, int b) {
+  P3D_WG_STAMP(4);
   int j = 0;
   while (j + 1 < mw.n && b >= mw.begin[j + 1]) ++j;
   const WgradLayer& l = mw.ly[j];
@@ -1514,6 +1515,9 @@ struct p3d_model {
   AdamFuse dp_af{};              // hyper-parameters of the last p3d_train_fwd_bwd_lr (p3d_adam_apply)
   bool alpha_ready = false;      // the last backward formed alpha_dev (p3d_adam_apply reads it)
   int wgrad_multi = 1;           // all layers' dW in one k_wgrad_multi launch (env P3D_WGRAD_MULTI)
+                                 // (measured and rejected, round 3: two adjacent 64x64 tiles per
+                                 // workgroup, 528 workgroups in one round instead of 768 + 288:
+                                 // 29.7 vs 28.4 us -- the launch is bound by its 148 MB HBM stream)
   int wgrad_attach = 0;          // fused train step: layer l + 1's dW + Adam tiles ride layer l's dgrad launch
                                  // (k_dgrad_wg; env P3D_WGRAD_ATTACH=1; bit-identical, measured slower:
                                  // 129.7 vs 126.3 us per cfg3 step -- the optimizer traffic slows the dgrad)

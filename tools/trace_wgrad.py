@@ -28,12 +28,15 @@ lib = _p3d.lib()
 lib.p3d_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(4096 * 8, np.uint64)
 assert lib.p3d_debug_trace(buf.ctypes.data, buf.size) == 0
-n = int(os.environ.get("NWG", "1056"))
-t = buf[4096:4096 + 8 * n].astype(np.int64).reshape(n, 8)[:, :4]
+n = int(os.environ.get("NWG", "1500"))
+t = buf[4096:4096 + 8 * n].astype(np.int64).reshape(n, 8)[:, :5]
+t = t[t[:, 4] > 0]                       # workgroups of the launch (slot 4: workgroup start)
+t = t[t[:, 4] >= t[:, 4].max() - 10000]  # (the last launch: within 100 us of its latest start)
+t[:, 0] = t[:, 4]                        # slot 0 = the workgroup's start (a pair's second tile re-stamps 0)
 t0 = t[:, 0].min()
 us = (t - t0) / 100.0
 q = lambda a: [round(float(np.quantile(a, f)), 2) for f in (0, 0.1, 0.5, 0.9, 1.0)]  # noqa: E731
-print(json.dumps({"start": q(us[:, 0]), "staged": q(us[:, 1]), "contracted": q(us[:, 2]), "done": q(us[:, 3]),
+print(json.dumps({"start": q(us[:, 0]), "staged_last_tile": q(us[:, 1]), "contracted": q(us[:, 2]), "done": q(us[:, 3]),
                   "stage_dur": q(us[:, 1] - us[:, 0]), "mfma_dur": q(us[:, 2] - us[:, 1]),
                   "adam_dur": q(us[:, 3] - us[:, 2]), "wg_dur": q(us[:, 3] - us[:, 0])}))
 # dispatch rounds: histogram of start times in 1-us bins
