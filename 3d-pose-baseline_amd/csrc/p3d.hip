@@ -252,7 +252,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
   }
 #endif
   // ---- epilogue operands issued before the GEMM so their latency overlaps it -------
-  float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4];
+  float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv[RS][4], tv[RS][4];
   uint64_t ctr = p.ctr;
   unsigned xtag = 0;
   if (w == 0) {
@@ -266,6 +266,9 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + 16 * s + 4 * q + r;
         rv[s][r] = p.res ? p.res[p3d_pk(row, cc, ngN)] : 0.f;
+        // fused MSE targets (training output layer): requested with the other epilogue
+        // operands, not after the contraction (one dependent round trip less)
+        tv[s][r] = (KIND == 2 && p.tgt && row < p.M) ? p.tgt[(int64_t)row * p.ldy + cc] : 0.f;
       }
   }
   const int ngt = p.K >> 4;
@@ -383,12 +386,11 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       if (q == 0 && cok) {
         p.mean_save[col] = mean;
         p.var_save[col] = var;
-        p.mmean[col] = mmu - (mmu - mean) * p.decay;
-        p.mvar[col] = mva - (mva - var) * p.decay;
+        p.mmean[col] = p3d_bn_moving(mmu, mean, p.decay);
+        p.mvar[col] = p3d_bn_moving(mva, var, p.decay);
       }
     }
-    inv = (1.0f / sqrtf(var + p.eps)) * gam;
-    shift = bet - mean * inv;
+    p3d_bn_affine(mean, var, p.eps, gam, bet, inv, shift);
   }
   if (trace) P3D_STAMP(3);
   float uu[RS][4];
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + 16 * s + 4 * q + r;
         if (cok && row < p.M) {
-          const float d = z[s][r] - p.tgt[(int64_t)row * p.ldy + col];
+          const float d = z[s][r] - (KIND == 2 ? tv[s][r] : p.tgt[(int64_t)row * p.ldy + col]);
           p.dy[(int64_t)row * p.lddy + col] = d * p.dscale;
           ls += d * d;
         }
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
       if (p.z_save) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
-      float y = p.bn == 4 ? p3d_bn_y(z[s][r], inv, shift) : p.bn ? z[s][r] * inv + shift : z[s][r];
+      float y = (p.bn == 4 || p.bn == 2) ? p3d_bn_y(z[s][r], inv, shift) : p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
       if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, uu[s][r]);
       if (p.res) y += rv[s][r];
@@ -1431,6 +1433,7 @@ struct p3d_model {
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
+  int in_whole = 0;           // BN-train input layer at B <= 64 as whole-batch workgroups (env P3D_IN_WHOLE)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -1811,6 +1814,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
+  if (const char* ev = getenv("P3D_IN_WHOLE")) m->in_whole = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
   {
     int dev = 0;
@@ -2079,6 +2083,15 @@ static XchgSite xchg_site(const p3d_model* m, int slot) {
 }
 
 static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
+  if (kind == 0 && a0.M <= 64 && a0.K == 32 && m->in_whole) {
+    // BN-train input layer at B <= 64: one workgroup holds all rows of its 16 columns (two
+    // waves, one k-group each), so the batch statistics are workgroup-local -- no row-tile
+    // exchange, no k_bn_fwd; the K = 32 contraction is too small to want more workgroups
+    ProfScope ps(m, "fwd_in_train_w");
+    go(ps, k_fwd<4, 2, 2, 2, false, true, 0>, dim3((a0.N + 15) / 16), dim3(128), st, a0);
+    LAUNCH_CHECK("k_fwd");
+    return P3D_OK;
+  }
   FwdArgs a = a0;
   a.bn = 3; a.bnpart = m->bnpart;
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
