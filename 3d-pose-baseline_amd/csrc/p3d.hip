@@ -386,11 +386,12 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       if (q == 0 && cok) {
         p.mean_save[col] = mean;
         p.var_save[col] = var;
-        p.mmean[col] = p3d_bn_moving(mmu, mean, p.decay);
-        p.mvar[col] = p3d_bn_moving(mva, var, p.decay);
+        p.mmean[col] = mmu - (mmu - mean) * p.decay;
+        p.mvar[col] = mva - (mva - var) * p.decay;
       }
     }
-    p3d_bn_affine(mean, var, p.eps, gam, bet, inv, shift);
+    inv = (1.0f / sqrtf(var + p.eps)) * gam;
+    shift = bet - mean * inv;
   }
   if (trace) P3D_STAMP(3);
   float uu[RS][4];
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
       const int row = m0 + 16 * s + 4 * q + r;
       if (row >= p.M) continue;
       if (p.z_save) p.z_save[p3d_pk(row, col, ngN)] = z[s][r];
-      float y = (p.bn == 4 || p.bn == 2) ? p3d_bn_y(z[s][r], inv, shift) : p.bn ? z[s][r] * inv + shift : z[s][r];
+      float y = p.bn == 4 ? p3d_bn_y(z[s][r], inv, shift) : p.bn ? z[s][r] * inv + shift : z[s][r];
       if (p.relu) y = fmaxf(y, 0.0f);
       if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, uu[s][r]);
       if (p.res) y += rv[s][r];
@@ -1433,7 +1434,8 @@ struct p3d_model {
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
-  int in_whole = 0;           // BN-train input layer at B <= 64 as whole-batch workgroups (env P3D_IN_WHOLE)
+  int in_train_wk = 8;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
+  int dgrad_out_wk = 8;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -1814,7 +1816,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
-  if (const char* ev = getenv("P3D_IN_WHOLE")) m->in_whole = atoi(ev);
+  if (const char* ev = getenv("P3D_IN_TRAIN_WK")) m->in_train_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_DGRAD_OUT_WK")) m->dgrad_out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
   {
     int dev = 0;
@@ -2083,15 +2086,6 @@ static XchgSite xchg_site(const p3d_model* m, int slot) {
 }
 
 static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
-  if (kind == 0 && a0.M <= 64 && a0.K == 32 && m->in_whole) {
-    // BN-train input layer at B <= 64: one workgroup holds all rows of its 16 columns (two
-    // waves, one k-group each), so the batch statistics are workgroup-local -- no row-tile
-    // exchange, no k_bn_fwd; the K = 32 contraction is too small to want more workgroups
-    ProfScope ps(m, "fwd_in_train_w");
-    go(ps, k_fwd<4, 2, 2, 2, false, true, 0>, dim3((a0.N + 15) / 16), dim3(128), st, a0);
-    LAUNCH_CHECK("k_fwd");
-    return P3D_OK;
-  }
   FwdArgs a = a0;
   a.bn = 3; a.bnpart = m->bnpart;
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
@@ -2101,7 +2095,9 @@ static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream
     ProfScope ps(m, tags[kind == 0 ? 0 : 1]);
     dim3 g = grid;
     if (m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
-    if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, g, dim3(512), st, a);
+    if (kind == 0 && m->in_train_wk == 2 && a.K <= 32) go(ps, k_fwd<1, 2, 1, 2, false, true, 0>, g, dim3(128), st, a);
+    else if (kind == 0 && m->in_train_wk == 4 && a.K <= 64) go(ps, k_fwd<1, 4, 1, 2, false, true, 0>, g, dim3(256), st, a);
+    else if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, g, dim3(512), st, a);
     else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, g, dim3(512), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
@@ -2988,7 +2984,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         } else {
           dim3 g = grid;
           if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
-          go(ps, k_dgrad<1, 8, 8, 2, false, 2>, g, dim3(512), st, a);
+          if (m->dgrad_out_wk == 4) go(ps, k_dgrad<1, 4, 4, 2, false, 2>, g, dim3(256), st, a);
+          else go(ps, k_dgrad<1, 8, 8, 2, false, 2>, g, dim3(512), st, a);
         }
       }
       LAUNCH_CHECK("k_dgrad");
