@@ -679,13 +679,20 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
   const bool cok = col < p.K;
   const int cc = cok ? col : p.K - 1;
   const int ngK = p.K >> 4;
-  if (p.alpha_out && bx == 0 && by == 0 && threadIdx.x == 0)
-    *p.alpha_out = p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
-  if (p.lossp && bx == 0 && by == 0 && threadIdx.x == 0) {
-    float l = 0.f;
-    for (int k = 0; k < p.nlossp; ++k) l += p.lossp[k];
-    p.loss[0] = l * p.loss_scale;
-  }
+  // the step's Adam alpha and the folded loss (tile (0, 0)): side outputs nothing in this launch
+  // reads, so with several waves the last one forms them after its share of the contraction
+  // (done first by wave 0 they delayed the tile's operand requests by their load round trip,
+  // and the whole launch by it, through the tile's exchange siblings)
+  auto side_outputs = [&]() {
+    if (p.alpha_out) *p.alpha_out = p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
+    if (p.lossp) {
+      float l = 0.f;
+      for (int k = 0; k < p.nlossp; ++k) l += p.lossp[k];
+      p.loss[0] = l * p.loss_scale;
+    }
+  };
+  constexpr bool side_late = WK >= 3;
+  if (!side_late && bx == 0 && by == 0 && threadIdx.x == 0) side_outputs();
   // prefetch the epilogue's per-column and per-element operands
   float mean = 0.f, var = 1.f, gam = 1.f, bet = 0.f, zz[RS][4], dr[RS][4];
   uint64_t ctr = p.ctr;
@@ -716,6 +723,7 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
   if (pubw) p3d_xchg_pub_reset(&xpub);
   if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) {
     if (pubw) p3d_xchg_publish(p.xs, &xpub, p.K, by, n0);
+    if (side_late && w == WK - 1 && lane == 0 && bx == 0 && by == 0) side_outputs();
     return;
   }
   const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
@@ -1434,8 +1442,8 @@ struct p3d_model {
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
-  int in_train_wk = 8;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
-  int dgrad_out_wk = 8;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
+  int in_train_wk = 2;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
+  int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
