@@ -379,6 +379,36 @@ def test_fused_train_step_bit_identical_to_unfused(residual, batch_norm, attach,
     plain.close()
 
 
+def test_small_launch_wave_counts_bit_identical(monkeypatch):
+    """The BN-train input layer on 2 waves and the output layer's dgrad on 4 (the defaults) give
+    the bits of the 8-wave forms (P3D_IN_TRAIN_WK / P3D_DGRAD_OUT_WK = 8): the extra waves hold
+    no k-group of these K = 32 / 48 contractions and only add zeros.  3 fused cfg3 train steps."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=6, bn_seed=7)
+    outs = []
+    for wk in (None, "8"):
+        if wk:
+            monkeypatch.setenv("P3D_IN_TRAIN_WK", wk)
+            monkeypatch.setenv("P3D_DGRAD_OUT_WK", wk)
+        m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_test", seed=9)
+        m.set_weights({**st.params, **st.moving})
+        rng = np.random.default_rng(13)
+        ys = []
+        for _ in range(3):
+            x = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+            t = torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda()
+            y = torch.empty((64, 48), device="cuda")
+            m.train_step_device(x, t, 0.5, out=y)
+            ys.append(y.clone())
+        torch.cuda.synchronize()
+        outs.append((ys, {k: m.flat[k].clone() for k in ("params", "moving", "adam_m", "adam_v")}))
+        m.close()
+    for a, b in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(a, b)
+    for k in outs[0][1]:
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k
+
+
 def test_tf_checkpoint_save_restore(tmp_path):
     """Saver.save writes a TensorFlow V2 checkpoint (checkpoint-N.index / .data-00000-of-00001
     + the `checkpoint` state file, tf_bundle.py) holding every tf.global_variables() name with
