@@ -1444,9 +1444,9 @@ struct p3d_model {
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   int in_train_wk = 2;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
   int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
-  int xchg_wk = 8;            // waves of the BN-train hidden exchange-form forward (env P3D_XCHG_WK: 8, 16;
-                              // 16 measured 8.6 vs 6.8 us)
-  int dgrad_wk = 16;          // waves of the hidden data-gradient launches (env P3D_DGRAD_WK: 16, 8)
+  int xchg_wk = 8;            // BN-train hidden exchange-form forward tiling (env P3D_XCHG_WK: 8 = 8 waves
+                              // with an 8-deep ring; 16 (16 waves, measured 8.6 vs 6.8 us), 84, 82: ring 4, 2)
+  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8, 162 = 16 with a 2-deep ring)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -2112,6 +2112,8 @@ static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream
     else if (kind == 0 && m->in_train_wk == 4 && a.K <= 64) go(ps, k_fwd<1, 4, 1, 2, false, true, 0>, g, dim3(256), st, a);
     else if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, g, dim3(512), st, a);
     else if (m->xchg_wk == 16) go(ps, k_fwd<1, 16, 4, 2, true, true, 1>, g, dim3(1024), st, a);
+    else if (m->xchg_wk == 84) go(ps, k_fwd<1, 8, 4, 2, true, true, 1>, g, dim3(512), st, a);
+    else if (m->xchg_wk == 82) go(ps, k_fwd<1, 8, 2, 2, true, true, 1>, g, dim3(512), st, a);
     else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, g, dim3(512), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
@@ -2997,6 +2999,7 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           // 16 waves (both BN forms, so they keep giving the same bits): 6.8 vs 7.0-7.1 us per
           // hidden dgrad (A/B, one box); the attached-wgrad form keeps k_dgrad_wg's 8-wave split
           if (m->dgrad_wk == 16 && !m->wgrad_attach) go(ps, k_dgrad<1, 16, 4, 2, true, 1>, g, dim3(1024), st, a);
+          else if (m->dgrad_wk == 162 && !m->wgrad_attach) go(ps, k_dgrad<1, 16, 2, 2, true, 1>, g, dim3(1024), st, a);
           else go(ps, k_dgrad<1, 8, 8, 2, true, 1>, g, dim3(512), st, a);
         } else {
           dim3 g = grid;
