@@ -89,6 +89,14 @@ SIGNATURES = [
     ("p3d_moments_workspace", c_int64, [c_int64, c_int32]),
     ("p3d_moments", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_crc32c", c_uint32, [c_void_p, c_int64, c_uint32]),
+    ("p3d_comm_load", c_int32, [c_char_p]),
+    ("p3d_comm_unique_id", c_int32, [c_void_p, c_int64]),
+    ("p3d_comm_create", c_int32, [c_void_p, c_int64, c_int32, c_int32, POINTER(c_void_p)]),
+    ("p3d_comm_destroy", c_int32, [c_void_p]),
+    ("p3d_comm_allreduce", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
+    ("p3d_dp_attach", c_int32, [c_void_p, c_void_p]),
+    ("p3d_train_step_dp", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_float, c_uint64, c_int64,
+                                    c_float, c_float, c_float, c_void_p, c_void_p]),
 ]
 
 

@@ -1422,6 +1422,7 @@ struct Layer {
 
 }  // namespace
 
+struct p3d_comm;
 struct p3d_model {
   p3d_cfg cfg;
   std::vector<Tensor> tensors;
@@ -1513,6 +1514,9 @@ struct p3d_model {
   float* serve_ecg = nullptr;      // k_serve6 epilogue-constant table (k_serve_prep), [layer][tile][48] + divisors
   bool serve_ec_dirty = true;      // parameters or moving statistics changed since the table was formed
   unsigned* serve_sync = nullptr;  // [k_serve6 bank 0 | bank 1 | k_serve5 bank | device epoch word ...]
+  int serve_delay = 0, serve_delay_xcc = 0;  // test hook (env P3D_SERVE_TEST_DELAY=n[,xcc]): on odd-numbered
+                                   // p3d_serve calls every workgroup on XCD xcc starts ~n x 3.4 us late
+  int64_t serve_calls = 0;
   int serve_fault = 0;             // test hook: the census waits for one workgroup more than the grid
                                    // (env P3D_SERVE_TEST_FAULT): every launch fails its census
   int serve_grid = 0;
@@ -1552,6 +1556,14 @@ struct p3d_model {
   int serve6_rt = 0;        // k_serve6 row tiles per unit, 0 = chosen per launch (env P3D_SERVE6_RT: 4 or 2)
   int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
   std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
+  // data-parallel step with the library's own all-reduce (p3d_dp.h)
+  p3d_comm* comm = nullptr;      // not owned (p3d_comm_create / p3d_comm_destroy)
+  hipStream_t cst = nullptr;     // comm stream (non-blocking), forked from / joined to the caller's stream
+  hipEvent_t cjoin = nullptr;    // join event of the comm-stream optimizer form (P3D_DP_ADAM=2)
+  std::vector<hipEvent_t> rev;   // per-bucket "all-reduce done" events
+  int dp_adam = 1;               // env P3D_DP_ADAM: 1 per-bucket optimizer on the compute stream behind its
+                                 // all-reduce, 0 one optimizer pass after the last bucket, 2 per bucket on the
+                                 // comm stream (round 3's form: slows the neighbouring dgrad launches)
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -1607,6 +1619,12 @@ void free_all(p3d_model* m) {
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
   for (hipEvent_t e : m->sev) (void)hipEventDestroy(e);
   m->sev.clear();
+  for (hipEvent_t e : m->rev) (void)hipEventDestroy(e);
+  m->rev.clear();
+  if (m->cjoin) (void)hipEventDestroy(m->cjoin);
+  m->cjoin = nullptr;
+  if (m->cst) (void)hipStreamDestroy(m->cst);
+  m->cst = nullptr;
   if (m->side) (void)hipStreamDestroy(m->side);
   m->side = nullptr;
 }
@@ -1850,8 +1868,13 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     m->serve_err = dv + 1;
   }
   if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
+  if (const char* ev = getenv("P3D_DP_ADAM")) m->dp_adam = atoi(ev);
   if (const char* ev = getenv("P3D_XCHG_REMAP")) m->xchg_remap = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_TEST_FAULT")) m->serve_fault = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE_TEST_DELAY")) {
+    m->serve_delay = atoi(ev);
+    if (const char* c = strchr(ev, ',')) m->serve_delay_xcc = atoi(c + 1) & 7;
+  }
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_ATTACH")) m->wgrad_attach = atoi(ev);
@@ -2639,6 +2662,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   a.sync = m->serve_sync; a.err = m->serve_err;
   a.epoch = m->serve_sync + 3 * P3D_SERVE_SYNC_WORDS;
   a.census_extra = m->serve_fault ? 1 : 0;
+  a.delay = (m->serve_delay > 0 && (m->serve_calls++ & 1) == 0) ? m->serve_delay : 0;
+  a.delay_xcc = m->serve_delay_xcc;
   a.max_groups = m->serve_groups;
   for (size_t l = 0; l < m->layers.size(); ++l) {
     const Layer& ly = m->layers[l];
@@ -3627,3 +3652,5 @@ extern "C" uint32_t p3d_crc32c(const void* data, int64_t n, uint32_t crc) {
   while (n-- > 0) c = (c >> 8) ^ tb.t[0][(c ^ *p++) & 0xFFu];
   return ~c;
 }
+
+#include "p3d_dp.h"

@@ -113,7 +113,8 @@ struct ServeArgs {
                        // of two consecutive banks (the launch picks one by *epoch)
   int* err;            // host-visible (pinned) error word: 1 = a bounded spin ran out, 2 = a placement
                        // the launch was not sized for
-  unsigned* epoch;     // k_serve6: launches so far (device-side, advanced by the launch itself)
+  unsigned* epoch;     // k_serve6: epoch (high 16 bits) | arrivals of the running launch (low 16 bits)
+  int delay, delay_xcc;  // k_serve6 test hook (P3D_SERVE_TEST_DELAY): the workgroups on XCD delay_xcc start late
   int census_extra;    // test hook: k_serve5's census waits for this many workgroups beyond the grid; k_serve6 takes it as a placement failure
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)

@@ -12,8 +12,8 @@
 // on the critical path and 4 phases, instead of 32 tiles and 8 phases.
 //
 // One launch per call: the sync words alternate between two banks picked on the device (the
-// launch reads an epoch word, uses bank epoch & 1, zeroes the other for the next launch, and one
-// workgroup advances the epoch at the end of its work, long after every workgroup read it),
+// launch reads an epoch word, uses bank epoch & 1, zeroes the other for the next launch; the last
+// workgroup to arrive advances the epoch, so all of a launch's workgroups read the same one),
 // so a launch needs no memset in front and captured graphs replay correctly.  The epilogue
 // constants come from a table k_serve_prep forms per parameter version.
 //
@@ -142,7 +142,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int xcc = (int)(xr & 7u), rx = (int)(blockIdx.x >> 3);
   unsigned ep = 0;
   if (tid == 0) {
-    ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (in flight)
+    // test hook (P3D_SERVE_TEST_DELAY): every workgroup of one XCD arrives ~delay x 3.4 us late
+    if (p.delay > 0 && xcc == p.delay_xcc)
+      for (int i = 0; i < p.delay; ++i) __builtin_amdgcn_s_sleep(127);
+    // arrival word: high 16 bits the launch epoch, low 16 bits this launch's arrivals so far.  The
+    // last workgroup to arrive resets the count and advances the epoch, so every workgroup of a
+    // launch reads the same epoch however late it starts, and the next launch (stream order: after
+    // this one completed) the next one.  (Round 3 advanced the epoch at the END of workgroup 0's
+    // work: a whole XCD group dispatched after workgroup 0 had finished read the advanced epoch,
+    // ran on the other bank and left its flags there for the next launch.)  One returning atomic
+    // per workgroup, in flight with the prologue's operand requests like the epoch read it replaces.
+    const unsigned v = __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ep = v >> 16;
+    if ((v & 0xFFFFu) == gridDim.x - 1u)
+      __hip_atomic_fetch_add(p.epoch, 0x10000u - gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool bad = (gridDim.x & 7u) != 0u || S < 1 || S > 8 || p.census_extra;
     sh[0] = (int)(((unsigned)xcc - blockIdx.x) & 7u);   // (trace: the launch's starting XCD)
     sh[2] = bad ? 1 : 0;
@@ -229,10 +242,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float qnan = __builtin_nanf("");
     for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < p.M * p.ND; e += (int64_t)gridDim.x * 256) p.y[e] = qnan;
   } else {
-  // workgroup 0 advances the epoch for the next launch at the END of its work (every other
-  // workgroup read it at its start, a launch's length earlier; a late one belongs to a group
-  // whose hand-offs time out and report)
-  const bool leader = tid == 0 && blockIdx.x == 0;
   if (gi < 0) {                              // a placement the host did not size this form for:
     if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     gi = p.nb;                               // the whole group reports instead of computing
@@ -643,6 +652,5 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
   }
-  if (leader) __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

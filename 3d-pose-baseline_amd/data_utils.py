@@ -172,15 +172,30 @@ class _Tree:
             self.npz = np.load(bpath, allow_pickle=False)
             self.names = list(self.npz.files)
 
+    def close(self):
+        if self.npz is not None:
+            self.npz.close()
+            self.npz = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     def glob(self, pattern):
         """Relative paths matching ``pattern`` (glob semantics on the archive's names; the
-        reference's glob.glob on a directory)."""
+        reference's glob.glob on a directory), sorted: the reference's order is whatever its
+        directory listing gave (src/data_utils.py:87,145), and it feeds the normalisation
+        statistics' vstack and the training-set order, so this build fixes it instead of
+        inheriting the archive's member order or the file system's (parity unpinned)."""
         if self.npz is None:
             base = os.path.join(self.bpath, "")
-            return [f[len(base):] if f.startswith(base) else f
-                    for f in glob.glob(os.path.join(self.bpath, pattern))]
+            return sorted(f[len(base):] if f.startswith(base) else f
+                          for f in glob.glob(os.path.join(self.bpath, pattern)))
         d, leaf = os.path.split(pattern)
-        return [n for n in self.names if os.path.dirname(n) == d and fnmatch.fnmatchcase(os.path.basename(n), leaf)]
+        return sorted(n for n in self.names
+                      if os.path.dirname(n) == d and fnmatch.fnmatchcase(os.path.basename(n), leaf))
 
     def read(self, rel, dataset):
         if self.npz is not None:
@@ -200,7 +215,11 @@ def load_data(bpath, subjects, actions, dim=3):
     subject and action for 3D, 8 for 2D."""
     if dim not in (2, 3):
         raise ValueError('dim must be 2 or 3')
-    tree = _Tree(bpath)
+    with _Tree(bpath) as tree:
+        return _load_data(tree, subjects, actions, dim)
+
+
+def _load_data(tree, subjects, actions, dim):
     data = {}
     for subj in subjects:
         for action in actions:
@@ -227,7 +246,11 @@ def load_stacked_hourglass(data_dir, subjects, actions):
     """{(subject, action, seqname + '-sh'): [n, 64]} from ``S<subj>/StackedHourglass/<action>*.h5``
     (src/data_utils.py:120-192): detections permuted to H3.6M order and scattered into the 64
     2D columns; 8 sequences per subject and action (7 for S11 Directions)."""
-    tree = _Tree(data_dir)
+    with _Tree(data_dir) as tree:
+        return _load_stacked_hourglass(tree, subjects, actions)
+
+
+def _load_stacked_hourglass(tree, subjects, actions):
     xs = np.flatnonzero(np.array([x != '' and x != 'Neck/Nose' for x in H36M_NAMES])) * 2
     cols = np.zeros(len(SH_NAMES) * 2, dtype=np.int32)
     cols[0::2], cols[1::2] = xs, xs + 1

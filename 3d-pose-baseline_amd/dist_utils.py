@@ -15,6 +15,8 @@ Everything here works on CPU tensors with the gloo backend too (tests/test_dist.
 """
 from __future__ import annotations
 
+import os
+
 
 def dist_state():
     """(initialized, rank, world) of the default process group."""
@@ -78,50 +80,31 @@ def plan_buckets(ranges, min_elems):
 
 
 def allreduce_mean_buckets_(t, buckets, wait_ready, comm_stream, after=None):
-    """Bucketed DP gradient average that overlaps the backward.
+    """Bucketed DP gradient average, host-staged (gloo: tests of several ranks on one GPU).
 
     For each bucket k (backward order), ``comm_stream`` waits for its gradient-ready event
-    (``wait_ready(k, stream_handle)``, p3d_stream_wait_grad),
-    then an async all-reduce(AVG) of that slice is issued from it (RCCL); the current
-    stream finally waits for all of them.  Every byte of ``t`` is reduced exactly once, so
-    the result equals ``allreduce_mean_`` (tests/test_gpu_dist.py).  Under gloo (tests:
-    several ranks on one GPU) each bucket is copied to the host on ``comm_stream`` after
-    its event -- the same event ordering, host-staged: a bucket read before its layer's
-    gradients are final would differ from the single all-reduce.  ``after(k, stream_handle)``
-    (optional) is issued on ``comm_stream`` behind bucket k's reduced slice -- the bucket's
-    optimizer (p3d_adam_apply_bucket) -- and the current stream then waits for ``comm_stream``.
-    """
+    (``wait_ready(k, stream_handle)``, p3d_stream_wait_grad), the slice is copied to the host,
+    all-reduced and copied back -- the event ordering of the device path (a bucket read before
+    its layers' gradients are final would differ from the single all-reduce).
+    ``after(k, stream_handle)`` (optional) is issued on ``comm_stream`` behind bucket k's reduced
+    slice -- the bucket's optimizer (p3d_adam_apply_bucket) -- and the current stream then waits
+    for ``comm_stream``.  Under RCCL the library reduces the buckets itself
+    (p3d_train_step_dp, native_comm below)."""
     import torch
     import torch.distributed as dist
-    if dist.get_backend() != "nccl":
-        world = dist.get_world_size()
-        with torch.cuda.stream(comm_stream):
-            for k, (lo, hi, _) in enumerate(buckets):
-                wait_ready(k, comm_stream.cuda_stream)
-                h = t[lo:hi].to("cpu")          # synchronous on comm_stream, after the event
-                dist.all_reduce(h, op=dist.ReduceOp.SUM)
-                h.div_(world)
-                t[lo:hi].copy_(h)
-                if after is not None:
-                    after(k, comm_stream.cuda_stream)
-        torch.cuda.current_stream().wait_stream(comm_stream)
-        return t
-    works = []
+    if dist.get_backend() == "nccl":
+        raise RuntimeError("allreduce_mean_buckets_: RCCL data parallelism runs in libp3d (p3d_train_step_dp)")
+    world = dist.get_world_size()
     with torch.cuda.stream(comm_stream):
         for k, (lo, hi, _) in enumerate(buckets):
             wait_ready(k, comm_stream.cuda_stream)
-            if after is None:
-                works.append(dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG, async_op=True))
-            else:
-                # a synchronous collective runs on the current stream (comm_stream) itself: the
-                # bucket's optimizer queues right behind it.  (An async one plus work.wait() from
-                # comm_stream crashed HIP graph capture at capture end.)
-                dist.all_reduce(t[lo:hi], op=dist.ReduceOp.AVG)
+            h = t[lo:hi].to("cpu")          # synchronous on comm_stream, after the event
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            h.div_(world)
+            t[lo:hi].copy_(h)
+            if after is not None:
                 after(k, comm_stream.cuda_stream)
-    if after is not None:
-        torch.cuda.current_stream().wait_stream(comm_stream)
-    for w in works:
-        w.wait()
+    torch.cuda.current_stream().wait_stream(comm_stream)
     return t
 
 
@@ -134,6 +117,60 @@ def allreduce_sum_(t):
         if h is not t:
             t.copy_(h)
     return t
+
+
+_NATIVE = {}
+
+
+def librccl_path():
+    """The librccl this process already uses (torch's bundled copy), for p3d_comm_load: one RCCL
+    per process."""
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so.1"
+
+
+def native_comm():
+    """The library-owned RCCL communicator over the default process group's ranks (p3d_comm,
+    include/p3d.h): rank 0 draws a unique id, it is broadcast over torch.distributed once, and
+    every rank joins.  Cached per (world, rank); the data-parallel step reduces over it inside
+    libp3d (p3d_train_step_dp), so a captured step holds no torch collective.
+    RCCL process groups only (one GPU per rank); gloo tests use the host-staged path."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    import _p3d
+    on, rank, world = dist_state()
+    if not on:
+        raise RuntimeError("native_comm: no process group")
+    key = (world, rank)
+    c = _NATIVE.get(key)
+    if c is not None:
+        return c
+    L = _p3d.lib()
+    _p3d.check(L.p3d_comm_load(librccl_path().encode()), "p3d_comm_load")
+    uid = (ctypes.c_uint8 * 128)()
+    if rank == 0:
+        _p3d.check(L.p3d_comm_unique_id(uid, 128), "p3d_comm_unique_id")
+    t = torch.tensor(list(bytes(uid)), dtype=torch.uint8,
+                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.broadcast(t, src=0)
+    ctypes.memmove(uid, bytes(t.cpu().tolist()), 128)
+    h = ctypes.c_void_p()
+    _p3d.check(L.p3d_comm_create(uid, 128, world, rank, ctypes.byref(h)), "p3d_comm_create")
+    _NATIVE[key] = h
+    return h
+
+
+def close_native_comms():
+    """Destroy the cached communicators (before destroy_process_group; every rank calls it)."""
+    import _p3d
+    import torch
+    if not _NATIVE:
+        return
+    torch.cuda.synchronize()
+    for k in list(_NATIVE):
+        _p3d.check(_p3d.lib().p3d_comm_destroy(_NATIVE.pop(k)), "p3d_comm_destroy")
 
 
 def broadcast_(tensors, src: int = 0):

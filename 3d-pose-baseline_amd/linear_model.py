@@ -128,7 +128,9 @@ class Saver:
         path = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
         self.model.sync_moving_stats()   # data parallel: one set of moving statistics
         self.model.torch.cuda.synchronize(self.model.device)
-        self.model.check_errors()        # never save the result of a failed in-launch exchange
+        # never save the result of a failed in-launch exchange -- on ANY rank: the flags are combined
+        # over the replicas first, so every rank raises together instead of some waiting in the barrier
+        self.model.check_errors(collective=True)
         if self.model.rank != 0:
             self._barrier()
             return path
@@ -496,18 +498,28 @@ class LinearModel(object):
         """Raise if a BN-train layer's in-launch exchange timed out (synchronises)."""
         check(lib().p3d_sync_check(self._h), "p3d_train")
 
-    def check_errors(self):
+    def check_errors(self, collective=False):
         """Raise P3DError if a kernel that has completed reported a failed in-launch
         synchronisation (BN-train exchange, serve census / hand-off).  No device round trip:
         the error words live in pinned host memory the kernels write (p3d_error_flags), so the
         callers check after a synchronisation they make anyway (loss read, output copy,
-        checkpoint save).  Reported once."""
+        checkpoint save).  Reported once.  ``collective=True`` (data parallel; every rank calls
+        it): the flags are OR-ed over the replicas first, so all ranks raise or none does."""
         import ctypes
         f = ctypes.c_int32(0)
         check(lib().p3d_error_flags(self._h, ctypes.byref(f), 0), "p3d_error_flags")
+        local = f.value
+        if collective and self.data_parallel:
+            import torch.distributed as dist
+            dev = self.device if dist.get_backend() == "nccl" else "cpu"
+            t = self.torch.tensor([local & 1, local & 2, local & 4], dtype=self.torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)    # per bit: the OR over the ranks
+            f = ctypes.c_int32(int(t.sum().item()))
         if f.value:
-            check(lib().p3d_error_flags(self._h, ctypes.byref(f), 1), "p3d_error_flags")
-            what = []
+            if local:
+                c = ctypes.c_int32(0)
+                check(lib().p3d_error_flags(self._h, ctypes.byref(c), 1), "p3d_error_flags")
+            what = [] if local else ["on another rank:"]
             if f.value & 1:
                 what.append("a BN-train exchange timed out (row-tile workgroups not all resident): the step's "
                             "batch statistics / gradients are invalid")
@@ -551,6 +563,16 @@ class LinearModel(object):
             # of the backward under RCCL), then TF1 Adam + re-pack + step advance in one launch
             if getattr(self, "_buckets", False) is False:   # first DP step: the default plan,
                 self.dp_buckets()                            # events on before the backward
+            if getattr(self, "_native", None) is not None:
+                # RCCL: the whole step inside the library -- the bucket all-reduces on its comm
+                # stream from its own communicator, each bucket's Adam behind its reduction
+                # (p3d_train_step_dp): no torch collective, so the step captures into one graph
+                check(lib().p3d_train_step_dp(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
+                                              self.rank * B, self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
+                      "p3d_train_step_dp")
+                self._step_host += 1
+                return loss_t, y
+            # gloo (tests: several ranks on one GPU): host-staged all-reduce between the library calls
             check(lib().p3d_train_fwd_bwd_lr(self._h, ptr(x), ptr(t), B, ptr(y), float(keep_prob), self.seed,
                                              self.rank * B, self.lr0, 100000.0, 0.96, ptr(loss_t), self.stream()),
                   "p3d_train_fwd_bwd_lr")
@@ -581,17 +603,22 @@ class LinearModel(object):
         overlaps the backward (env P3D_DP_BUCKET_MB, default 8 MB: at cfg2 two buckets, {output,
         hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two weight-gradient launches;
         RCCL by default, gloo -- host-staged, for tests of several ranks on one GPU -- when
-        gloo=True).  Must be called before a backward is issued.  Returns the bucket plan
-        [(begin, end, lowest layer)] in backward order."""
+        gloo=True).  Under RCCL the model is attached to the library's own communicator
+        (dist_utils.native_comm, p3d_dp_attach) and every DP step is one p3d_train_step_dp.
+        Must be called before a backward is issued (all ranks together: the first call builds
+        the communicator).  Returns the bucket plan [(begin, end, lowest layer)] in backward order."""
         import ctypes
         import torch.distributed as dist
         if bucket_mb is None:
             bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "8"))
-        # each bucket's optimizer right behind its all-reduce (p3d_adam_apply_bucket), overlapping
-        # the rest of the backward; P3D_DP_BUCKET_ADAM=0: one p3d_adam_apply after the last bucket
+        nccl = self.data_parallel and dist.is_initialized() and dist.get_backend() == "nccl"
+        if nccl and getattr(self, "_native", None) is None:
+            self._native = dist_utils.native_comm()
+            check(lib().p3d_dp_attach(self._h, self._native), "p3d_dp_attach")
+        # gloo path: each bucket's optimizer right behind its host all-reduce (p3d_adam_apply_bucket);
+        # P3D_DP_BUCKET_ADAM=0: one p3d_adam_apply after the last bucket (RCCL: env P3D_DP_ADAM)
         self._bucket_adam = os.environ.get("P3D_DP_BUCKET_ADAM", "1") != "0"
-        on = (bucket_mb > 0 and self.data_parallel and dist.is_initialized()
-              and (dist.get_backend() == "nccl" or gloo))
+        on = bucket_mb > 0 and self.data_parallel and dist.is_initialized() and (nccl or gloo)
         self._buckets = None
         if on:
             ranges = []
@@ -602,7 +629,8 @@ class LinearModel(object):
             self._buckets = dist_utils.plan_buckets(ranges, int(bucket_mb * (1 << 20)) // 4)
             lo = (ctypes.c_int32 * len(self._buckets))(*[b[2] for b in self._buckets])
             check(lib().p3d_grad_buckets(self._h, len(self._buckets), lo), "p3d_grad_buckets")
-            self._comm = self.torch.cuda.Stream(device=self.device)
+            if not nccl:
+                self._comm = self.torch.cuda.Stream(device=self.device)
         else:
             check(lib().p3d_grad_buckets(self._h, 0, None), "p3d_grad_buckets")
         return self._buckets

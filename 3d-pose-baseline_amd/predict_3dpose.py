@@ -138,14 +138,17 @@ def create_model(session, actions, batch_size, flags=None, load_exact=False):
     # checkpoint-N.index exists, then restores the checkpoint the directory's `checkpoint` file
     # names as the latest (ckpt.model_checkpoint_path, :180) -- not necessarily N.  Pass
     # load_exact=True (a keyword of this build) to restore checkpoint-N itself.
+    # A directory of an earlier build's checkpoint-N.npz files has no `checkpoint` state file:
+    # there N itself is restored.
     import tf_bundle
     latest = tf_bundle.read_checkpoint_state(tdir)
-    if latest is None:
-        raise ValueError("Checkpoint directory {0} does not seem to hold a checkpoint".format(tdir))
     ck = os.path.join(tdir, "checkpoint-{0}".format(flags.load))
-    if not (os.path.isfile(ck + ".index") or os.path.isfile(ck + ".npz")):
+    have = os.path.isfile(ck + ".index") or os.path.isfile(ck + ".npz")
+    if latest is None and not have:
+        raise ValueError("Checkpoint directory {0} does not seem to hold a checkpoint".format(tdir))
+    if not have:
         raise ValueError("Asked to load checkpoint {0}, but it does not seem to exist".format(flags.load))
-    path = ck if load_exact else latest
+    path = ck if (load_exact or latest is None) else latest
     print("Loading model {0}".format(os.path.basename(ck)))
     model.saver.restore(session, path)
     return model

@@ -1049,6 +1049,52 @@ def cpu_data_baseline(seconds):
             "sample": "%d camera-poses (4 sequences x 2600 frames x 4 cameras per pass), %.1f s" % (done, dt)}
 
 
+def run_dp1_child(args, timeout=300):
+    """Run the 1-rank data-parallel train leg as `bench.py --dp1-child` (a fresh process; the
+    caller has not initialised the GPU) and return its JSON, or {"error": ...}."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--dp1-child", "--train-steps", str(args.train_steps),
+           "--dp-bucket-mb", str(args.dp_bucket_mb), "--keep", str(args.keep)]
+    if args.train_eager:
+        cmd.append("--train-eager")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "dp1 child timed out after %d s" % timeout}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode == 0 and lines:
+        try:
+            return json.loads(lines[-1])
+        except ValueError:
+            pass
+    return {"error": "dp1 child rc %d" % r.returncode, "stderr_tail": r.stderr[-1500:]}
+
+
+def dp1_child(args, json_fd):
+    """The 1-rank RCCL data-parallel step (bench_train(dp=True) on a world-1 process group): the
+    whole DP step -- buckets, the library's RCCL all-reduce, per-bucket Adam -- as HIP graphs."""
+    import torch.distributed as dist
+    import dist_utils
+    import torch
+    torch.cuda.set_device(0)
+    init_world1_group()
+    dv, ddt, droof, dmode = bench_train(args, 0, 1, steps=args.train_steps, warmup=64, dp=True)
+    out = {"workload": "the data-parallel step (fwd + bwd with %g MB gradient buckets, one weight-gradient launch "
+                       "each, RCCL all-reduce from libp3d's own communicator on its comm stream, each bucket's TF1 "
+                       "Adam + re-pack behind its all-reduce on the compute stream, step advance in the last; "
+                       "1-rank group: the reduction is the identity)" % args.dp_bucket_mb,
+           "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
+           "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
+           "event_pair_avg_us": droof.get("event_pair_avg_us")}
+    dist_utils.close_native_comms()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
+    return 0
+
+
 def build_arg_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1081,6 +1127,7 @@ def build_arg_parser():
     ap.add_argument("--data-reps", type=int, default=10)
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
+    ap.add_argument("--dp1-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="print the N-rank launch command --gpus N > 1 would run, and exit")
     return ap
@@ -1101,6 +1148,15 @@ def main():
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.dp1_child:
+        return dp1_child(args, json_fd)
+    # the data-parallel step's form on a 1-rank RCCL group (what every rank runs at N > 1), in a
+    # child process that runs BEFORE this one touches the GPU: whatever happens to it (a fault, an
+    # abort from a runtime thread) cannot take the headline line with it
+    dp1 = None
+    if (args.mode == "infer" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_dp1
+            and args.train_steps > 0):
+        dp1 = run_dp1_child(args)
     rank, world, local = setup_dist()
     train = single = sweep = api = data = stress = lat = None
     chain = None
@@ -1131,22 +1187,8 @@ def main():
                          "roofline": troof}
             except Exception as exc:  # report, never lose the headline line
                 train = {"error": repr(exc)[:300]}
-            if world == 1 and not args.no_dp1 and "error" not in train:
-                try:   # the data-parallel step's form on a 1-rank RCCL group (what each rank runs at N > 1)
-                    own = init_world1_group()
-                    dv, ddt, droof, dmode = bench_train(args, rank, world, steps=args.train_steps, warmup=64, dp=True)
-                    train["dp_form_1rank"] = {
-                        "workload": "the data-parallel step (fwd + bwd with %g MB gradient buckets, one weight-gradient "
-                                    "launch each, RCCL all-reduce(AVG) on a 1-rank group, each bucket's TF1 Adam + "
-                                    "re-pack behind its all-reduce, step advance in the last)" % args.dp_bucket_mb,
-                        "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
-                        "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
-                        "event_pair_avg_us": droof.get("event_pair_avg_us")}
-                    if own:
-                        import torch.distributed as dist
-                        dist.destroy_process_group()
-                except Exception as exc:
-                    train["dp_form_1rank"] = {"error": repr(exc)[:300]}
+            if dp1 is not None:
+                train["dp_form_1rank"] = dp1
             if world > 1 and args.dp_bucket_mb > 0 and "error" not in train:
                 try:   # the same steps with one all-reduce after the backward (no overlap)
                     sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=0)
@@ -1243,6 +1285,8 @@ def main():
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         import torch.distributed as dist
+        import dist_utils
+        dist_utils.close_native_comms()
         dist.destroy_process_group()
 
 

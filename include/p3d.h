@@ -205,6 +205,37 @@ int p3d_adam_apply(p3d_model* m, void* stream);
  * P3D_ERR_STATE (they take p3d_adam_apply). */
 int p3d_adam_apply_bucket(p3d_model* m, int32_t bucket, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Data-parallel training with the gradient all-reduce issued by this library (the
+ * reference is single-process, its step is one session.run of the train op, src/linear_model.py:
+ * 230-237, with one optimizer step per batch, :137-145).  librccl is resolved at run time from
+ * the library the process already uses (pass torch's librccl path; NULL = "librccl.so.1"):
+ * libp3d.so has no link-time dependency on it.  The ranks build a communicator from a unique id
+ * rank 0 draws and broadcasts over the caller's own channel (torch.distributed), attach it to a
+ * model, and p3d_train_step_dp then runs the whole DP step -- forward, backward, the bucketed
+ * all-reduce of the flat gradient on a library-owned stream overlapping the backward, TF1 Adam +
+ * re-pack, step advance -- holding no object of the caller's runtime, so one HIP graph captures it
+ * whole.  The reduction is the replica mean (one rank: the identity).
+ * ------------------------------------------------------------------------------------- */
+typedef struct p3d_comm p3d_comm;
+int p3d_comm_load(const char* librccl_path);
+int p3d_comm_unique_id(uint8_t* id, int64_t id_len /* >= 128 */);
+int p3d_comm_create(const uint8_t* id, int64_t id_len, int32_t nranks, int32_t rank, p3d_comm** out);
+int p3d_comm_destroy(p3d_comm* c);
+/* in-place all-reduce of n elements (dtype P3D_DTYPE_F32 / F64; op 0 sum, 1 mean, 2 max) on `stream` */
+int p3d_comm_allreduce(p3d_comm* c, void* buf, int64_t n, int32_t dtype, int32_t op, void* stream);
+/* the communicator the model's data-parallel step reduces over (NULL detaches; not owned) */
+int p3d_dp_attach(p3d_model* m, p3d_comm* c);
+/* One data-parallel training step.  With gradient buckets (p3d_grad_buckets) bucket k's
+ * all-reduce runs on the library's comm stream as soon as the backward recorded its event and its
+ * TF1 Adam follows on `stream` (env P3D_DP_ADAM: 1 default; 0 one optimizer pass after the last
+ * bucket; 2 each bucket's optimizer on the comm stream); without buckets one all-reduce after the
+ * backward.  Arguments as p3d_train_fwd_bwd_lr.  Graph-capturable (the comm stream is forked from
+ * and joined to `stream`). */
+int p3d_train_step_dp(p3d_model* m, const float* x, const float* t, int64_t B, float* y, float keep_prob,
+                      uint64_t seed, int64_t row_offset, float lr0, float decay_steps, float decay_rate,
+                      float* loss_dev, void* stream);
+
 /* One whole single-GPU TF1 training step (linear_model.py:225-237): p3d_train_fwd_bwd then
  * the TF1 Adam update, global_step += 1.  By default (env P3D_FUSE_ADAM=1 at p3d_create) the
  * update runs inside the batched weight-gradient launch (k_wgrad_multi: no separate optimizer

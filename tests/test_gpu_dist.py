@@ -113,6 +113,8 @@ def _worker_buckets(rank, world, port, out):
             m.close()
         res["mn%d" % max_norm] = np.stack([ms["bucketed"], ms["single"], ms["local"]])
     np.savez(out, **res)
+    import dist_utils
+    dist_utils.close_native_comms()
     dist.destroy_process_group()
 
 
@@ -366,6 +368,8 @@ def _worker_rccl_graph(rank, world, port, out):
         res[tag + "_step"] = np.array(m.get_step()[0])
         m.close()
     np.savez(out, **res)
+    import dist_utils
+    dist_utils.close_native_comms()
     dist.destroy_process_group()
 
 
@@ -380,3 +384,71 @@ def test_dp_rccl_step_graph_capture(tmp_path):
     np.testing.assert_array_equal(r["graph"], r["eager"])
     np.testing.assert_array_equal(r["graph"], r["local"])
     assert int(r["graph_step"]) == int(r["eager_step"]) == 3
+
+
+def _worker_rccl_capture_linger(rank, world, port, out):
+    """BENCH_r03's abort, reproduced deterministically: eager DP steps, a torch collective still in
+    flight, then -- with no synchronisation in between -- the capture of the DP step, and replays
+    spread over ~3 s (many ProcessGroupNCCL watchdog polls) before the bits are compared."""
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    import dist_utils
+    import linear_model
+    rng = np.random.default_rng(91)
+    x0 = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+    t0 = torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda()
+    reps, per = 12, 2
+    res = {}
+    for tag in ("graph", "eager", "local"):
+        m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_dpl", seed=6,
+                                     data_parallel=(tag != "local"))
+        m.initialize(seed=14)
+        if tag != "local":
+            m.dp_buckets(8)
+        xb, tb = x0.clone(), t0.clone()
+        for _ in range(3):
+            m.train_step_device(xb, tb, 0.5)
+        if tag == "graph":
+            w = torch.ones(1 << 16, device="cuda")
+            work = dist.all_reduce(w, async_op=True)        # a torch Work the watchdog still holds
+            s0 = torch.cuda.Stream()
+            s0.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s0, capture_error_mode="thread_local"):
+                for _ in range(per):
+                    m.train_step_device(xb, tb, 0.5)
+            m._step_host -= per
+            torch.cuda.current_stream().wait_stream(s0)
+            for _ in range(reps):
+                g.replay()
+                torch.cuda.synchronize()
+                time.sleep(0.25)
+            work.wait()
+        else:
+            for _ in range(reps * per):
+                m.train_step_device(xb, tb, 0.5)
+        torch.cuda.synchronize()
+        m.check_errors()
+        res[tag] = m.flat["params"].cpu().numpy().copy()
+        res[tag + "_step"] = np.array(m.get_step()[0])
+        m.close()
+    dist_utils.close_native_comms()
+    np.savez(out, **res)
+    dist.destroy_process_group()
+
+
+def test_dp_rccl_capture_after_eager_lingers(tmp_path):
+    """The RCCL DP step (libp3d's own communicator, p3d_train_step_dp) captured right after eager DP
+    steps with a torch collective in flight, then replayed over ~3 s: the process survives the
+    watchdog's polls, and graph == eager == the fused single-GPU step bit for bit (1-rank group)."""
+    out = str(tmp_path / "l.npz")
+    mp.spawn(_worker_rccl_capture_linger, args=(1, free_port(), out), nprocs=1, join=True)
+    r = np.load(out)
+    np.testing.assert_array_equal(r["graph"], r["eager"])
+    np.testing.assert_array_equal(r["graph"], r["local"])
+    assert int(r["graph_step"]) == int(r["eager_step"]) == 3 + 24

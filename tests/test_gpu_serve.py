@@ -356,3 +356,35 @@ def test_serve_graph_replay_follows_inputs_and_parameters():
     close(y.cpu().numpy(), ro)
     del g
     m.close()
+
+
+@pytest.mark.parametrize("xcc", [0, 3, 7])
+def test_serve6_late_xcd_group_keeps_launch_epochs(monkeypatch, xcc):
+    """Advisor r3 (high): k_serve6 picks its sync-word bank from a device epoch word.  Round 3
+    advanced the epoch at the end of workgroup 0's work, so a whole XCD group that started after
+    workgroup 0 had finished (possible with max_groups = 1: workgroup 0 often idles) read the next
+    epoch, ran on the other bank and left its flags there -- the NEXT launch's hand-offs then passed
+    on stale flags.  Now the last workgroup to arrive advances the epoch.  Test hook
+    P3D_SERVE_TEST_DELAY=n,xcc: on every other call all workgroups of XCD xcc start ~n x 3.4 us
+    late; the launches alternate delayed / on time and every output must equal an undelayed
+    model's bits."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    monkeypatch.setenv("P3D_SERVE_TEST_DELAY", "300,%d" % xcc)
+    monkeypatch.setenv("P3D_SERVE_GROUPS", "1")
+    st, m = make(cfg)
+    monkeypatch.delenv("P3D_SERVE_TEST_DELAY")
+    monkeypatch.delenv("P3D_SERVE_GROUPS")
+    _, ref = make(cfg)
+    rng = np.random.default_rng(40 + xcc)
+    B = 64 * 20
+    for call in range(6):
+        x = torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)).cuda()
+        y = m.serve_device(x)
+        y0 = ref.serve_device(x)
+        torch.cuda.synchronize()
+        m.serve_check()
+        assert torch.equal(y, y0), "launch %d (delayed=%s) differs" % (call, call % 2 == 0)
+    ro, _ = ref_mlp.forward(st, x.cpu().numpy(), False, 1.0, 0, 0, 0)
+    close(y.cpu().numpy(), ro)
+    m.close()
+    ref.close()

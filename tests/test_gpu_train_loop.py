@@ -74,6 +74,34 @@ def test_create_model_load_restores_latest(tmp_path):
         predict_3dpose.create_model(None, ["All"], bad.batch_size, bad)
 
 
+def test_create_model_load_npz_only_directory(tmp_path):
+    """Advisor r3 (low): a directory holding only an earlier build's checkpoint-N.npz (no
+    `checkpoint` state file) restores N itself; a missing N still raises ValueError."""
+    import checkpoint_io
+    args = ["--linear_size", "256", "--num_layers", "1", "--residual", "--batch_norm",
+            "--learning_rate", "1e-3", "--train_dir", str(tmp_path)]
+    flags = predict_3dpose.build_parser().parse_args(args)
+    m = predict_3dpose.create_model(None, ["All"], flags.batch_size, flags)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 0.5, isTraining=True)
+    want = m.get_state()
+    m.close()
+    d = predict_3dpose.train_dir_for(flags)
+    os.makedirs(d, exist_ok=True)
+    np.savez(os.path.join(d, "checkpoint-3.npz"), **want)
+    lflags = predict_3dpose.build_parser().parse_args(args + ["--load", "3"])
+    m2 = predict_3dpose.create_model(None, ["All"], lflags.batch_size, lflags)
+    got = m2.get_state()
+    for k in checkpoint_io.global_order(m2.param_table):
+        np.testing.assert_array_equal(np.asarray(got[k], np.float64), np.asarray(want[k], np.float64), err_msg=k)
+    assert m2.get_step()[0] == 3
+    m2.close()
+    with pytest.raises(ValueError, match="does not seem to"):
+        bad = predict_3dpose.build_parser().parse_args(args + ["--load", "4"])
+        predict_3dpose.create_model(None, ["All"], bad.batch_size, bad)
+
+
 @pytest.mark.parametrize("use_sh", [False, True])
 def test_train_from_archives(tmp_path, use_sh):
     """train() on files (src/predict_3dpose.py:194-208): cameras, 3D poses and 2D inputs read
