@@ -43,6 +43,7 @@ SIGNATURES = [
     ("p3d_flat_ptr", c_int32, [c_void_p, c_int32, POINTER(c_void_p), POINTER(c_int64)]),
     ("p3d_params_updated", c_int32, [c_void_p, c_void_p]),
     ("p3d_params_changed", c_int32, [c_void_p]),
+    ("p3d_params_sync", c_int32, [c_void_p, c_void_p]),
     ("p3d_forward", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,
                               c_uint64, c_int64, c_void_p]),
     ("p3d_forward_ex", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,

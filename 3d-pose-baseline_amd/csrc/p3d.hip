@@ -66,6 +66,7 @@ struct AdamFuse {
   float lr_host;        // >= 0: use as lr; < 0: device exponential decay of lr0
   float lr0, decay_steps, decay_rate;
   float b1, b2, eps;
+  int wsrc;             // 1: weights read from their Wd copy, the TF-layout master not written (p3d_adam_tile64)
 };
 
 __device__ __forceinline__ float p3d_adam_alpha(const StepState* st, float lr_host, float lr0, float decay_steps,
@@ -81,11 +82,22 @@ __device__ __forceinline__ float p3d_adam_alpha(const StepState* st, float lr_ho
 // g comes from `g` (global) or, when g == nullptr, from tile[k - k0][n - n0] (the fused
 // weight-gradient kernel); tile ends holding the updated weights.  Bit-identical updates
 // either way (same gradient values, same p3d_adam1).
+//
+// wsrc = 1 (every optimizer of a model without --max_norm): the weights are read from their Wd copy
+// -- the TF layout tiled: Wd element (k, n) is lane (k & 15) + 16 ((n & 15) >> 2), component n & 3
+// of 16x16 tile (k >> 4, n >> 4), a permutation, so the values are the master's bit for bit -- and
+// the TF-layout master is NOT written: 4 of the 32 / 36 bytes per weight element the optimizer moves.
+// The master is re-derived from Wd when something reads it (p3d_params_sync).
+__device__ __forceinline__ int64_t p3d_wd_at(int k, int n, int ngd) {
+  return ((int64_t)((k >> 4) * ngd + (n >> 4)) * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
+}
 __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* g, int64_t off, int K, int N,
                                                 int k0, int n0, float* w, float* m, float* v, float* wd,
-                                                float* wf, float alpha, float omb1, float omb2, float eps) {
+                                                float* wf, float alpha, float omb1, float omb2, float eps,
+                                                int wsrc = 0) {
   const int tid = threadIdx.x;
   const bool vec = (N & 3) == 0;
+  const int ngd_ = ((N + 15) & ~15) >> 4;
   if (vec) {
     // all four rows' w / m / v (and g) requested before the first update, from clamped (always
     // valid) addresses, stores after: a load inside the per-row range branch made every row a
@@ -98,7 +110,7 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
       const int k = k0 + r, n = n0 + c;
       ok[it] = k < K && n < N;
       const int64_t base = ok[it] ? off + (int64_t)k * N + n : off;
-      ww[it] = *(const f32x4*)(w + base);
+      ww[it] = wsrc ? *(const f32x4*)(wd + (ok[it] ? p3d_wd_at(k, n, ngd_) : 0)) : *(const f32x4*)(w + base);
       mm[it] = *(const f32x4*)(m + base);
       vv[it] = *(const f32x4*)(v + base);
       if (g) gg[it] = *(const f32x4*)(g + base);
@@ -116,7 +128,8 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
           p3d_adam1(w1, m1, v1, gg[it][e], alpha, omb1, omb2, eps);
           ww[it][e] = w1; mm[it][e] = m1; vv[it][e] = v1; wn[e] = w1;
         }
-        *(f32x4*)(w + base) = ww[it]; *(f32x4*)(m + base) = mm[it]; *(f32x4*)(v + base) = vv[it];
+        if (!wsrc) *(f32x4*)(w + base) = ww[it];
+        *(f32x4*)(m + base) = mm[it]; *(f32x4*)(v + base) = vv[it];
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];   // each thread rewrites only what it read
@@ -132,9 +145,10 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (n + e < N) {
-            float ww = w[base + e], mm = m[base + e], vv = v[base + e];
+            float ww = wsrc ? wd[p3d_wd_at(k, n + e, ngd_)] : w[base + e], mm = m[base + e], vv = v[base + e];
             p3d_adam1(ww, mm, vv, g ? g[base + e] : tile[r][c + e], alpha, omb1, omb2, eps);
-            w[base + e] = ww; m[base + e] = mm; v[base + e] = vv;
+            if (!wsrc) w[base + e] = ww;
+            m[base + e] = mm; v[base + e] = vv;
             wn[e] = ww;
           }
       }
@@ -1068,7 +1082,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
       for (int r = 0; r < 4; ++r) tile[16 * w + 4 * q + r][16 * s + i] = acc[s][r];
     __syncthreads();
     p3d_adam_tile64(tile, nullptr, p.woff, p.K, p.N, k0, n0, p.w, p.m, p.v, p.wd, p.wf, alpha,
-                    1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps);
+                    1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps, p.af.wsrc);
 #ifdef P3D_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1188,6 +1202,7 @@ struct AdamArgs {
   float lr0, decay_steps, decay_rate;
   float b1, b2, eps;
   int wblocks;          // blocks spent on weight tiles (one 64x64 tile each)
+  int wsrc;             // weights from Wd, TF-layout master not written (p3d_adam_tile64)
 };
 
 // One 64x64 weight tile per 256-thread block: 16 threads x float4 per 256-B row segment;
@@ -1224,7 +1239,7 @@ __global__ __launch_bounds__(256) void k_adam_pack(AdamArgs a, AdamTable tb) {
     const int local = tile_id - tb.tile_begin[wi];
     const int k0 = (local / tnc) * 64, n0 = (local % tnc) * 64;
     p3d_adam_tile64(tile, a.g, tb.off[wi], K, N, k0, n0, a.w, a.m, a.v, a.wpk + tb.wd[wi], a.wpk + tb.wf[wi],
-                    alpha, omb1, omb2, a.eps);
+                    alpha, omb1, omb2, a.eps, a.wsrc);
   } else {
     const int chunk = blockIdx.x - a.wblocks;
     if (chunk < tb.vbegin[tb.nv]) {
@@ -1271,6 +1286,26 @@ struct PackTable {
   int64_t src[P3D_MAX_W], dstf[P3D_MAX_W], dstd[P3D_MAX_W];  // element offsets
   int64_t begin[P3D_MAX_W + 1];  // float4 prefix over (Wf + Wd) outputs
 };
+
+// The TF-layout master of every weight re-derived from its Wd copy (p3d_params_sync): a pure
+// permutation, so the master equals what an optimizer writing it would have written, bit for bit.
+struct UnpackTable {
+  int n;
+  int N[P3D_MAX_W];
+  int64_t src[P3D_MAX_W], dstd[P3D_MAX_W];
+  int64_t begin[P3D_MAX_W + 1];   // element prefix over the weights' K x N masters
+};
+__global__ __launch_bounds__(256) void k_unpack_w(const float* __restrict__ wpk, float* __restrict__ params,
+                                                  UnpackTable ut) {
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= ut.begin[ut.n]) return;
+  int t = 0;
+  while (t + 1 < ut.n && o >= ut.begin[t + 1]) ++t;
+  const int N = ut.N[t], ngd = ((N + 15) & ~15) >> 4;
+  const int64_t e = o - ut.begin[t];
+  const int k = (int)(e / N), n = (int)(e % N);
+  params[ut.src[t] + e] = wpk[ut.dstd[t] + p3d_wd_at(k, n, ngd)];
+}
 
 __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ params, float* __restrict__ wpk, PackTable pt) {
   const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1477,6 +1512,14 @@ struct p3d_model {
   float* wsq = nullptr;       // [nW] ||W||^2
   float* gw = nullptr;        // [nW] <G,W>
   PackTable pt;
+  UnpackTable ut;
+  // --max_norm off: every optimizer reads the weights from Wd and leaves the TF-layout master
+  // unwritten (AdamFuse::wsrc); w_stale marks a master behind Wd until p3d_params_sync (env
+  // P3D_W_MASTER=1: the optimizers write the master, as before round 4)
+  int w_pk = 1;
+  bool w_stale = false;
+  bool w_sticky = false;         // an optimizer was captured into a graph: its replays leave the masters
+                                 // behind without this host code seeing it, so every sync re-derives them
   AdamTable at;
   int adam_blocks = 0;
   StepState* dstate = nullptr;  // device: global_step, beta powers, arrival counter
@@ -1596,6 +1639,14 @@ template <typename F, typename... A>
 void go(const ProfScope& ps, F k, dim3 grid, dim3 block, hipStream_t st, A... args) {
   if (ps.on) hipExtLaunchKernelGGL(k, grid, block, 0, st, ps.e0, ps.e1, 0, args...);
   else k<<<grid, block, 0, st>>>(args...);
+}
+
+// An optimizer is issued that leaves the TF-layout masters behind Wd (AdamFuse::wsrc).
+void mark_w_stale(p3d_model* m, hipStream_t st) {
+  if (!m->w_pk) return;
+  m->w_stale = true;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) m->w_sticky = true;
 }
 
 void free_all(p3d_model* m) {
@@ -1747,6 +1798,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   // packed-weight buffer and tables
   m->pt.n = 0;
+  m->ut.n = 0;
+  m->ut.begin[0] = 0;
   m->wtab.n = 0;
   int64_t f4 = 0;
   for (size_t l = 0; l < m->layers.size(); ++l) {
@@ -1760,6 +1813,9 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     m->pt.src[t] = ly.w; m->pt.dstf[t] = ly.wf; m->pt.dstd[t] = ly.wd;
     m->pt.begin[t] = f4;
     f4 += 2 * (int64_t)NP * K / 4;
+    m->ut.N[t] = N; m->ut.src[t] = ly.w; m->ut.dstd[t] = ly.wd;
+    m->ut.begin[t + 1] = m->ut.begin[t] + (int64_t)K * N;
+    m->ut.n = t + 1;
     ly.widx = t;
     m->wtab.off[t] = ly.w;
     m->wtab.len[t] = (int64_t)K * N;
@@ -1869,6 +1925,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
   if (const char* ev = getenv("P3D_DP_ADAM")) m->dp_adam = atoi(ev);
+  if (const char* ev = getenv("P3D_W_MASTER")) m->w_pk = atoi(ev) ? 0 : 1;
+  if (m->cfg.max_norm) m->w_pk = 0;   // (||W||^2 of the max-norm scale is summed over the master)
   if (const char* ev = getenv("P3D_XCHG_REMAP")) m->xchg_remap = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_TEST_FAULT")) m->serve_fault = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_TEST_DELAY")) {
@@ -2025,8 +2083,30 @@ static int refresh_derived(p3d_model* m, hipStream_t st) {
   return P3D_OK;
 }
 
+// The TF-layout weight masters, re-derived from Wd if an optimizer left them behind (w_stale).
+// (mark_w_stale is defined next to the model: the optimizers call it when they skip the masters.)
+static int ensure_w(p3d_model* m, hipStream_t st) {
+  if (!m->w_stale && !m->w_sticky) return P3D_OK;
+  const int64_t n = m->ut.begin[m->ut.n];
+  {
+    ProfScope ps(m, "unpack_w");
+    go(ps, k_unpack_w, dim3((unsigned)((n + 255) / 256)), dim3(256), st, (const float*)m->wpk, m->flat[0], m->ut);
+  }
+  LAUNCH_CHECK("k_unpack_w");
+  m->w_stale = false;
+  return P3D_OK;
+}
+
+extern "C" int p3d_params_sync(p3d_model* m, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "null model");
+  return ensure_w(m, (hipStream_t)stream);
+}
+
 extern "C" int p3d_params_updated(p3d_model* m, void* stream) {
   if (!m) return fail(P3D_ERR_ARG, "null model");
+  // the host wrote the masters it holds: they must not have been behind Wd (it syncs first)
+  if (m->w_stale) return fail(P3D_ERR_STATE, "p3d_params_updated: weight masters were stale (p3d_params_sync "
+                                             "before writing parameters)");
   return refresh_derived(m, (hipStream_t)stream);
 }
 
@@ -3246,6 +3326,8 @@ extern "C" int p3d_adam_apply_bucket(p3d_model* m, int32_t bucket, void* stream)
   a.wpk = m->wpk; a.st = m->dstate;
   a.lr_host = -2.0f; a.lr0 = m->dp_af.lr0; a.decay_steps = m->dp_af.decay_steps; a.decay_rate = m->dp_af.decay_rate;
   a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
+  a.wsrc = m->w_pk;
+  mark_w_stale(m, st);
   a.wblocks = m->bat[bucket].tile_begin[m->bat[bucket].nw];
   a.alpha_dev = m->alpha_dev;
   a.advance = last ? m->dstate : nullptr;
@@ -3276,6 +3358,8 @@ extern "C" int p3d_train_step(p3d_model* m, const float* x, const float* t, int6
   AdamFuse af{};
   af.st = m->dstate; af.lr_host = -1.0f; af.lr0 = lr0; af.decay_steps = decay_steps; af.decay_rate = decay_rate;
   af.b1 = 0.9f; af.b2 = 0.999f; af.eps = 1e-8f;
+  af.wsrc = m->w_pk;
+  mark_w_stale(m, st);
   m->fuse_adam = &af;
   const int rc = p3d_train_fwd_bwd(m, x, t, B, y, keep_prob, seed, 0, loss_dev, stream);
   m->fuse_adam = nullptr;
@@ -3295,6 +3379,8 @@ static int adam_launch(p3d_model* m, float lr_host, float lr0, float steps, floa
   a.wpk = m->wpk; a.st = m->dstate;
   a.lr_host = lr_host; a.lr0 = lr0; a.decay_steps = steps; a.decay_rate = rate;
   a.b1 = 0.9f; a.b2 = 0.999f; a.eps = 1e-8f;
+  a.wsrc = m->w_pk;
+  mark_w_stale(m, st);
   a.wblocks = m->at.tile_begin[m->at.nw];
   const bool pre = lr_host == -2.0f;   // alpha formed by the backward (p3d_adam_apply): advance in-launch
   if (pre) { a.alpha_dev = m->alpha_dev; a.advance = m->dstate; }

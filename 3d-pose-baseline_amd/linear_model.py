@@ -178,6 +178,21 @@ class Saver:
             self.model.set_state({k: z[k] for k in z.files})
 
 
+class _FlatViews(dict):
+    """The model's flat device buffers by name; reading "params" first brings the weight
+    masters up to date (LinearModel.sync_params), so a view taken after training steps holds
+    the current weights."""
+
+    def __init__(self, model):
+        super().__init__()
+        self._model = model
+
+    def __getitem__(self, key):
+        if key == "params":
+            self._model.sync_params()
+        return dict.__getitem__(self, key)
+
+
 class LinearModel(object):
     """A simple Linear+RELU model (src/linear_model.py:31), on MI355X HIP kernels."""
 
@@ -267,13 +282,13 @@ class LinearModel(object):
             check(L.p3d_param_info(self._h, i, _p3d.ctypes.byref(name), _p3d.ctypes.byref(numel),
                                    _p3d.ctypes.byref(kind), _p3d.ctypes.byref(off)), "p3d_param_info")
             self.param_table.append((name.value.decode(), int(numel.value), int(kind.value), int(off.value)))
-        self.flat = {}
+        self.flat = _FlatViews(self)
         idx = self.device.index
         for which, key in enumerate(("params", "grads", "adam_m", "adam_v", "moving")):
             p = _p3d.c_void_p()
             ne = _p3d.c_int64()
             check(L.p3d_flat_ptr(self._h, which, _p3d.ctypes.byref(p), _p3d.ctypes.byref(ne)), "p3d_flat_ptr")
-            self.flat[key] = _p3d.device_view(p.value, (ne.value,), idx) if ne.value > 0 else None
+            dict.__setitem__(self.flat, key, _p3d.device_view(p.value, (ne.value,), idx) if ne.value > 0 else None)
         self._shapes = {}
         for name, numel, kind, off in self.param_table:
             self._shapes[name] = self._shape_of(name, numel)
@@ -308,6 +323,13 @@ class LinearModel(object):
 
     def stream(self):
         return _p3d.stream_handle()
+
+    def sync_params(self):
+        """The TF-layout weight masters up to date on the current stream (p3d_params_sync): the
+        optimizers of a model without --max_norm leave them behind the packed copies the kernels
+        read; every host read or write of the parameters goes through here first
+        (``variable``, ``get_weights``, ``set_weights``, ``flat["params"]``)."""
+        check(lib().p3d_params_sync(self._h, self.stream()), "p3d_params_sync")
 
     def params_updated(self):
         check(lib().p3d_params_updated(self._h, self.stream()), "p3d_params_updated")
@@ -349,6 +371,7 @@ class LinearModel(object):
     def set_weights(self, arrays: dict):
         """Write TF-named arrays (any subset) into device memory, then refresh layouts."""
         torch = self.torch
+        self.sync_params()   # a subset: the other masters must be current before the re-pack
         for name, val in arrays.items():
             v = self.variable(name)
             a = np.asarray(val, dtype=np.float32).reshape(v.shape)
@@ -409,6 +432,7 @@ class LinearModel(object):
 
     def broadcast_parameters(self):
         """Rank 0's variables to every rank (start of data-parallel training)."""
+        self.sync_params()
         dist_utils.broadcast_([self.flat[k] for k in ("params", "moving", "adam_m", "adam_v")], src=0)
         self.params_updated()
 

@@ -86,6 +86,14 @@ int p3d_flat_ptr(p3d_model* m, int32_t which /*0 params,1 grads,2 adam_m,3 adam_
  * p3d_flat_ptr (refreshes derived device layouts, e.g. transposed weights). */
 int p3d_params_updated(p3d_model* m, void* stream);
 
+/* Bring the TF-layout weight masters (params buffer, p3d_param_ptr) up to date on `stream`.
+ * The optimizers of a model without --max_norm read each weight from its packed data-gradient
+ * copy and do not write the TF-layout master (4 of the 32 bytes per weight element of the fused
+ * step's optimizer); call this before the host reads or writes weights through
+ * p3d_param_ptr / p3d_flat_ptr(0).  No device work when the masters are current.
+ * p3d_params_updated refuses (P3D_ERR_STATE) while they are behind. */
+int p3d_params_sync(p3d_model* m, void* stream);
+
 /* The parameters changed on the device without this library's host code issuing the change
  * (e.g. a replayed HIP graph of training steps, LinearModel.step's cached training graph):
  * host-scheduled derived tables (k_serve6's epilogue constants) are re-formed at their next

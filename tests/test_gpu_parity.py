@@ -679,3 +679,42 @@ def test_step_training_graph_bit_identical_to_eager(monkeypatch):
         np.testing.assert_array_equal(oa, ob)
     for k in sa:
         np.testing.assert_array_equal(np.asarray(sa[k]), np.asarray(sb[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("dp", [False, True])
+def test_optimizer_from_packed_weights_bit_identical(monkeypatch, dp):
+    """Round 4: without --max_norm every optimizer reads the weights from their packed Wd copy and
+    leaves the TF-layout master unwritten (re-derived on demand, p3d_params_sync).  Against the
+    form that writes the master (P3D_W_MASTER=1): 4 training steps -- the fused single-GPU step, or
+    the data-parallel form's separate optimizer (p3d_train_fwd_bwd_lr + p3d_adam_apply) -- give the
+    same bits in every variable and Adam slot, the masters read back after a captured-graph replay
+    included (the replays' updates are seen without any host call in between)."""
+    import _p3d
+    res = {}
+    for tag in ("master", "packed"):
+        if tag == "master":
+            monkeypatch.setenv("P3D_W_MASTER", "1")
+        m = linear_model.LinearModel(256, 2, True, True, False, 64, 1e-3, "/tmp/p3d_wpk", seed=3, max_batch=64)
+        monkeypatch.delenv("P3D_W_MASTER", raising=False)
+        m.initialize(seed=9)
+        rng = np.random.default_rng(5)
+        xs = [torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda() for _ in range(4)]
+        ts = [torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda() for _ in range(4)]
+        y = torch.empty((64, 48), device="cuda")
+        loss = torch.empty(1, device="cuda")
+        for i in range(3):
+            if dp:
+                _p3d.check(_p3d.lib().p3d_train_fwd_bwd_lr(m._h, _p3d.ptr(xs[i]), _p3d.ptr(ts[i]), 64, _p3d.ptr(y), 0.5,
+                                                           m.seed, 0, 1e-3, 100000.0, 0.96, _p3d.ptr(loss), m.stream()))
+                _p3d.check(_p3d.lib().p3d_adam_apply(m._h, m.stream()))
+            else:
+                m.train_step_device(xs[i], ts[i], 0.5)
+        if not dp:   # one more step as a captured graph, replayed; the masters must follow it
+            xb, tb = xs[3].clone(), ts[3].clone()
+            step = m.train_step_graph(xb, tb, 0.5)
+            step()
+        torch.cuda.synchronize()
+        res[tag] = {k: v.copy() for k, v in m.get_state().items()}
+        m.close()
+    for k, v in res["master"].items():
+        np.testing.assert_array_equal(np.asarray(res["packed"][k]), np.asarray(v), err_msg=k)

@@ -3,6 +3,7 @@
 // over back-to-back launches.  Build: tools/bf16_dev.sh; driver: tools/bf16_dev.py.
 #include "../3d-pose-baseline_amd/csrc/p3d_kernels.h"
 #include "../3d-pose-baseline_amd/csrc/p3d_bf16.h"
+#include "bf16_dev_kernels.h"
 
 extern "C" int dev_pack_x(const float* x, int M, int K, unsigned short* out) {
   const int items = (M / 16) * (K / 32) * 64;
