@@ -461,6 +461,37 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
 }
 
 // =====================================================================================
+// Training output layer as split-K partials (round 4).  The fused-MSE output layer (N = 48, 12
+// tiles at B = 64) ran as 12 workgroups of 8 waves: 12 CUs each taking in 128 KB while 244 idled
+// (6.3 us).  Here every (tile, K eighth) is its own one-wave workgroup (96 at B = 64): wave w of
+// the 8-wave k_fwd becomes workgroup (ct, rt, w), same k-groups, same MFMA chains, in the
+// transposed-accumulator form (p3d_core SWAP: the same products in the same order, lane (i, q)
+// holding row 16 rt + i, columns 4q .. 4q+3 -- the A-fragment layout of the data gradient).  The
+// output layer's data-gradient launch sums the 8 partials in wave order (k_fwd's association, so
+// y and dy are bit-identical), adds the bias, forms y, dy = 2(y - t)/(B D) and the loss partials,
+// and contracts dy with W^T straight from registers (p3d_dgrad_body, BwdArgs::opart).
+// =====================================================================================
+struct OutPartArgs {
+  const float* X;     // packed [M, K] (the last hidden layer's output)
+  const float* Wf;    // the output layer's forward operand
+  int M, K;
+  float* part;        // [R][NT][8] 1 KB tiles
+};
+template <int DEPTH>
+__global__ __launch_bounds__(64) void k_out_part(OutPartArgs p) {
+  const int lane = threadIdx.x;
+  const int ct = blockIdx.x, rt = blockIdx.y, sl = blockIdx.z;
+  const int ngt = p.K >> 4;
+  const int gb = (ngt * sl) / 8, ge = (ngt * (sl + 1)) / 8;
+  f32x4 acc[2][1];
+  acc[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  p3d_core<1, DEPTH, 2, true, true>(p.X, 0, ngt, p.M, 16 * rt, p.Wf, ngt, ct, gb, ge, acc);
+  acc[0][0] += acc[1][0];
+  ((f32x4*)p.part)[(((int64_t)rt * gridDim.x + ct) * 8 + sl) * 64 + lane] = acc[0][0];
+}
+
+// =====================================================================================
 // Inference layer in the transposed-accumulator form (p3d_core SWAP): lane (i, q) ends
 // holding row 16s + i, columns n0 + 4q .. +3 -- one float4 per operand of the epilogue
 // (bias, eval BN, residual, packed output: one 1 KB wave store per tile) and one Philox
@@ -677,6 +708,12 @@ struct BwdArgs {
   XchgSite xs; int xchg;          // with bnpart: exchange form (p3d_xchg.h) -- dz, dgamma, dbeta here
   int remap_gy;                   // > 0: 1-D grid of (K/16) * remap_gy blocks (p3d_sibling_remap)
   float* alpha_out; AdamFuse af;  // fused Adam: tile (0, 0) stores the step's alpha for later launches
+  // output layer from split-K partials (k_out_part): A = dy formed here, not loaded (dZ unused)
+  const float* opart; int ont;    //   partials [R][ont][8] and the output layer's column tiles
+  const float* obias; const float* otgt; int64_t oldt;   // bias [N], targets row-major
+  float* oy; int64_t oldy;        //   y out (row-major, the caller's), written by column tile 0
+  float* ody; int64_t oldd;       //   dy out (row-major, for the output layer's weight gradient)
+  float odscale; float* olossp;   //   2 / (B N); per-(row tile, column tile) sum of (y - t)^2
 };
 
 // RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
@@ -731,7 +768,47 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
   for (int a = 0; a < NACC; ++a)
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, m0, p.Wd, ngt, ct, gb, ge, acc);
+  if (KIND == 2 && RS == 1 && p.opart) {
+    // the output layer's dy from its split-K partials (k_out_part), one k-group = one output column
+    // tile per wave: partials summed in wave order, bias, y, dy, loss partial; then dy x W^T
+    const float mxo = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
+    const int row = m0 + i;
+    const int rt = m0 >> 4;
+    for (int g = gb; g < ge; ++g) {
+      const f32x4* pp = (const f32x4*)p.opart + (((int64_t)rt * p.ont + g) * 8) * 64 + lane;
+      f32x4 zs = pp[0];
+#pragma unroll
+      for (int sl = 1; sl < 8; ++sl) zs += pp[sl * 64];
+      const int c0 = 16 * g + 4 * q;
+      f32x4 a4, t4;
+      float ls = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t4[e] = (row < p.M && c0 + e < p.N) ? p.otgt[(int64_t)row * p.oldt + c0 + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = row < p.M && c0 + e < p.N;
+        const float z = (p.wsq ? zs[e] / mxo : zs[e]) + (c0 + e < p.N ? p.obias[c0 + e] : 0.f);
+        const float d = z - t4[e];
+        a4[e] = ok ? d * p.odscale : 0.f;
+        if (ok) ls += d * d;
+        if (ok && bx == 0) {
+          p.oy[(int64_t)row * p.oldy + c0 + e] = z;
+          p.ody[(int64_t)row * p.oldd + c0 + e] = a4[e];
+        }
+      }
+      if (bx == 0) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+        if (lane == 0) p.olossp[g + p.ont * rt] = ls;
+      }
+      const f32x4 rb = ((const f32x4*)p.Wd)[((int64_t)ct * ngt + g) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[e % NACC][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], rb[e], acc[e % NACC][0], 0, 0, 0);
+    }
+  } else {
+    p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, m0, p.Wd, ngt, ct, gb, ge, acc);
+  }
   __shared__ XchgPub xpub;                  // exchange form: wave 0 posts its column sums, wave 1 publishes
   const bool pubw = WK > 1 && p.xchg && p.prev && p.bn && w == 1;
   if (pubw) p3d_xchg_pub_reset(&xpub);
@@ -1477,6 +1554,11 @@ struct p3d_model {
   int adam_in_wgrad = 1;      // env P3D_FUSE_ADAM (default 1): p3d_train_step applies Adam inside k_wgrad_multi
                               // (bit-identical; measured slower than k_adam_pack at cfg3)
   float* dybuf = nullptr;     // [max_batch, output_size]: dy of the fused MSE
+  int out_part = 1;           // training output layer as split-K partials + dy in its dgrad (env P3D_OUT_PART)
+  float* opart = nullptr;     // [16 row tiles][4 column tiles][8] 1 KB partials (k_out_part)
+  bool opart_pending = false; // the last training forward left the output layer to the backward's first launch
+  const float* opart_t = nullptr;   // its targets and y (row-major, the caller's)
+  float* opart_y = nullptr;
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   int in_train_wk = 2;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
   int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
@@ -1656,6 +1738,7 @@ void free_all(p3d_model* m) {
   if (m->wpk) (void)hipFree(m->wpk);
   if (m->ws) (void)hipFree(m->ws);
   if (m->scratch) (void)hipFree(m->scratch);
+  if (m->opart) (void)hipFree(m->opart);
   if (m->dstate) (void)hipFree(m->dstate);
   if (m->wbf) (void)hipFree(m->wbf);
   if (m->aff) (void)hipFree(m->aff);
@@ -1891,6 +1974,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
                             pad64((int64_t)c.max_batch * ((c.output_size + 15) / 16 * 16));
   if ((e = hipMalloc(&m->scratch, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
   if ((e = hipMemset(m->scratch, 0, scratch_n * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMalloc(&m->opart, (size_t)16 * 4 * 8 * 256 * sizeof(float))) != hipSuccess) return cleanup(e);
+  if (const char* ev = getenv("P3D_OUT_PART")) m->out_part = atoi(ev);
   if (const char* ev = getenv("P3D_INFER_WK")) m->infer_wk = atoi(ev);
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
   if (const char* ev = getenv("P3D_FWD_T")) m->fwd_t = atoi(ev);
@@ -2453,10 +2538,19 @@ extern "C" int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y,
 
 // tgt != null (training): the output layer also forms dy = 2(y - t)/(B*D) into m->dybuf and
 // per-workgroup loss partials into m->lossp (p3d_train_fwd_bwd).
+// The training output layer as split-K partials (k_out_part) with y / dy / loss formed by the
+// backward's first launch: B <= 256 rows, N <= 64, the split BN-train kernels, a hidden layer
+// whose data gradient folds the loss afterwards (num_layers >= 1).
+static bool out_part_ok(const p3d_model* m, int64_t B) {
+  return m->out_part && m->train_split && B <= 256 && m->cfg.output_size <= 64 && m->layers.size() >= 3 &&
+         m->dgrad_out_wk == 4;
+}
+
 static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32_t training, float keep_prob,
                         uint64_t seed, uint64_t ctr, int64_t row_offset, int64_t ws_row, void* stream,
                         const float* tgt) {
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_forward: null argument");
+  m->opart_pending = false;
   const p3d_cfg& c = m->cfg;
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_forward: batch must be positive");
   if (ws_row < 0 || ws_row % 16 != 0) return fail(P3D_ERR_ARG, "p3d_forward_ex: ws_row must be a multiple of 16");
@@ -2512,6 +2606,21 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
       m->nlossp = (int)(((ly.N + 15) / 16) * ((B + 15) / 16));
     }
     const int kind = (l == 0) ? 0 : (last ? 2 : 1);
+    if (last && tgt && out_part_ok(m, B)) {
+      // split-K partials; y, dy and the loss partials are formed by the backward's first launch
+      OutPartArgs o{};
+      o.X = in; o.Wf = a.Wf; o.M = (int)B; o.K = ly.K; o.part = m->opart;
+      {
+        ProfScope ps(m, "fwd_out_part");
+        go(ps, k_out_part<8>, dim3((unsigned)((ly.N + 15) / 16), (unsigned)((B + 15) / 16), 8u), dim3(64), st, o);
+      }
+      LAUNCH_CHECK("k_out_part");
+      m->opart_pending = true;
+      m->opart_t = tgt;
+      m->opart_y = y;
+      in = a.Y;
+      continue;
+    }
 #ifdef P3D_DIAG_SKIP_IN   // diagnostic builds only (tools/): drop the input-layer launch
     if (!training && l == 0) { in = a.Y; continue; }
 #endif
@@ -2937,6 +3046,14 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   const int nl = (int)m->layers.size();
   float* grads = m->flat[1];
   const float* params = m->flat[0];
+  // the training forward left the output layer as split-K partials (k_out_part): the first data-
+  // gradient launch forms y, dy (into dybuf, where the output layer's weight gradient reads it)
+  // and the loss partials
+  const bool opart = m->opart_pending && dy == m->dybuf;
+  if (m->opart_pending && !opart)
+    return fail(P3D_ERR_STATE, "p3d_backward: the last training forward deferred its output layer to "
+                               "p3d_train_fwd_bwd's backward");
+  m->opart_pending = false;
   const float* dz_cur = dy;   // gradient wrt z of the current layer l
   bool dz_pk = false;         // dy is row-major; every later dz is packed
   int dsel = 0;
@@ -3066,9 +3183,18 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         if (l - 1 >= 1) a.draw = m->dout[dsel];
       }
     }
-    if (is_out && m->loss_dst) {
+    // the forward's loss partials are folded by the first backward launch -- or, when that launch
+    // forms them itself (output layer from split-K partials), by the next one
+    if (m->loss_dst && (opart ? l == nl - 2 : is_out)) {
       a.lossp = m->lossp; a.nlossp = m->nlossp; a.loss = m->loss_dst;
-      a.loss_scale = 1.0f / (float)(B * ly.N);
+      a.loss_scale = 1.0f / (float)(B * m->layers[nl - 1].N);
+    }
+    if (is_out && opart) {
+      a.opart = m->opart; a.ont = (ly.N + 15) / 16;
+      a.obias = params + ly.b; a.otgt = m->opart_t; a.oldt = ly.N;
+      a.oy = m->opart_y; a.oldy = ly.N;
+      a.ody = m->dybuf; a.oldd = np_out;
+      a.odscale = (1.0f / (float)(B * ly.N)) * 2.0f; a.olossp = m->lossp;
     }
     a.prev = 1;
     a.bn = pv.bn;

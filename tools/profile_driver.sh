@@ -1,15 +1,17 @@
 #!/bin/bash
 # Profiles of the driver's headline command (run on the GPU box from the repo root):
 #   1. rocprofv3 --kernel-trace --stats of `python3 bench.py --gpus 1 --steps 20 --warmup 5`
+#      (with --no-dp1: the 1-rank data-parallel leg runs in a child process of its own, profiled in 4)
 #   2. two separate PMC passes (FETCH_SIZE, WRITE_SIZE) of the serve path alone at 20 steps
 #      per launch (tools/pmc_traffic.py turns them into HBM bytes per launch)
 #   3. the same for the cfg3 training step (bench.py --mode train)
+#   4. kernel stats of the 1-rank data-parallel step (bench.py --dp1-child)
 # Every step under its own time limit; the script stops at the first failure.
 set -e
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_under_rocprof.json" 2> "$OUT/bench_under_rocprof.err"
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-dp1 > "$OUT/bench_under_rocprof.json" 2> "$OUT/bench_under_rocprof.err"
 SERVE="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-streams --no-eval --no-data --no-api --no-stress --train-steps 0 --no-cpu"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- $SERVE > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- $SERVE > "$OUT/write.json" 2> "$OUT/write.err"
@@ -18,4 +20,7 @@ TRAIN="python3 bench.py --gpus 1 --mode train --steps 64 --warmup 16 --no-cpu"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train_trace" -o run -- $TRAIN > "$OUT/train_under_rocprof.json" 2> "$OUT/train_under_rocprof.err"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/train_fetch" -o run -- $TRAIN > "$OUT/train_fetch.json" 2> "$OUT/train_fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/train_write" -o run -- $TRAIN > "$OUT/train_write.json" 2> "$OUT/train_write.err"
+# 4. the data-parallel step's form on a 1-rank RCCL group (what every rank runs at N > 1)
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dp1_trace" -o run -- \
+    python3 bench.py --dp1-child --train-steps 400 > "$OUT/dp1_under_rocprof.json" 2> "$OUT/dp1_under_rocprof.err"
 echo profile-done
