@@ -775,36 +775,48 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
     const int row = m0 + i;
     const int rt = m0 >> 4;
     for (int g = gb; g < ge; ++g) {
+      // every operand requested before anything is stored (a store ahead of a load of another
+      // array keeps the compiler from hoisting the load: one more round trip)
+      const f32x4 rb = ((const f32x4*)p.Wd)[((int64_t)ct * ngt + g) * 64 + lane];
       const f32x4* pp = (const f32x4*)p.opart + (((int64_t)rt * p.ont + g) * 8) * 64 + lane;
-      f32x4 zs = pp[0];
+      f32x4 pv[8];
 #pragma unroll
-      for (int sl = 1; sl < 8; ++sl) zs += pp[sl * 64];
+      for (int sl = 0; sl < 8; ++sl) pv[sl] = pp[sl * 64];
       const int c0 = 16 * g + 4 * q;
-      f32x4 a4, t4;
-      float ls = 0.f;
+      f32x4 t4, b4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t4[e] = (row < p.M && c0 + e < p.N) ? p.otgt[(int64_t)row * p.oldt + c0 + e] : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const bool okc = c0 + e < p.N;
+        t4[e] = (row < p.M && okc) ? p.otgt[(int64_t)(row < p.M ? row : 0) * p.oldt + c0 + e] : 0.f;
+        b4[e] = okc ? p.obias[c0 + e] : 0.f;
+      }
+      f32x4 zs = pv[0];
+#pragma unroll
+      for (int sl = 1; sl < 8; ++sl) zs += pv[sl];
+      f32x4 a4, z4;
+      float ls = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool ok = row < p.M && c0 + e < p.N;
-        const float z = (p.wsq ? zs[e] / mxo : zs[e]) + (c0 + e < p.N ? p.obias[c0 + e] : 0.f);
-        const float d = z - t4[e];
+        z4[e] = (p.wsq ? zs[e] / mxo : zs[e]) + b4[e];
+        const float d = z4[e] - t4[e];
         a4[e] = ok ? d * p.odscale : 0.f;
         if (ok) ls += d * d;
-        if (ok && bx == 0) {
-          p.oy[(int64_t)row * p.oldy + c0 + e] = z;
-          p.ody[(int64_t)row * p.oldd + c0 + e] = a4[e];
-        }
       }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[e % NACC][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], rb[e], acc[e % NACC][0], 0, 0, 0);
       if (bx == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (row < p.M && c0 + e < p.N) {
+            p.oy[(int64_t)row * p.oldy + c0 + e] = z4[e];
+            p.ody[(int64_t)row * p.oldd + c0 + e] = a4[e];
+          }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
         if (lane == 0) p.olossp[g + p.ont * rt] = ls;
       }
-      const f32x4 rb = ((const f32x4*)p.Wd)[((int64_t)ct * ngt + g) * 64 + lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc[e % NACC][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], rb[e], acc[e % NACC][0], 0, 0, 0);
     }
   } else {
     p3d_core<RS, DEPTH, NACC, APK>(p.dZ, p.ldz, ngt, p.M, m0, p.Wd, ngt, ct, gb, ge, acc);

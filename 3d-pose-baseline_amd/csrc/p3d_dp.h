@@ -25,8 +25,8 @@
 // so bucket k's all-reduce overlaps the data gradients of the layers below it, while every
 // optimizer launch stays on the compute queue (round 3 measured a comm-queue optimizer slowing
 // every neighbouring dgrad launch: 155 vs 107 us per step at one rank; P3D_DP_ADAM=2 keeps that
-// form).  One rank: the reduction is the identity (sum of one replica; RCCL enqueues nothing for an
-// in-place sum on a 1-rank communicator), N > 1: ncclAvg (RCCL pre-multiplies each contribution by
+// form).  One rank: the reduction is the identity (the mean of one replica), so the step issues no
+// collective and forks no comm stream -- the same launches in the same order otherwise; N > 1: ncclAvg (RCCL pre-multiplies each contribution by
 // 1/N; for N a power of two exactly the sum / N the host-staged gloo path computes).
 #pragma once
 #include <dlfcn.h>
@@ -182,8 +182,18 @@ extern "C" int p3d_train_step_dp(p3d_model* m, const float* x, const float* t, i
   const bool bucketed = nb > 0 && !m->cfg.max_norm && m->wgrad_multi && (int)m->bucket_lo.size() == nb &&
                         (int)m->bat.size() == nb;
   if (!bucketed) {
-    if ((rc = dp_allreduce(m, m->flat[1], m->n_flat, st))) return rc;
+    if (m->comm->nranks > 1 && (rc = dp_allreduce(m, m->flat[1], m->n_flat, st))) return rc;
     return p3d_adam_apply(m, stream);
+  }
+  if (m->comm->nranks == 1) {
+    // one replica: the mean of the gradients is the gradient itself and RCCL enqueues nothing for
+    // it, so no comm-stream branch either (a forked branch in a captured graph puts its edges on
+    // another hardware queue and slowed every launch of the step by 0.4-0.7 us, r04 A/B): each
+    // bucket's optimizer follows on the compute stream
+    if (m->dp_adam == 0) return p3d_adam_apply(m, stream);
+    for (int k = 0; k < nb; ++k)
+      if ((rc = p3d_adam_apply_bucket(m, k, stream))) return rc;
+    return P3D_OK;
   }
   if ((int)m->rev.size() != nb) {
     for (hipEvent_t e : m->rev) HIP_TRY(hipEventDestroy(e));

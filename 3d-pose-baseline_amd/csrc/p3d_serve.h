@@ -60,7 +60,7 @@
 #define P3D_SERVE_FLAG0 256
 #define P3D_SERVE_SYNC_WORDS (P3D_SERVE_FLAG0 + 64 * 64)   // flags of up to 64 groups (k_serve6 S <= 8)
 // the model's serve sync allocation: k_serve6 banks 0 / 1 (group flags), the k_serve5 bank, then
-// k_serve6's device epoch word (bank = epoch & 1) on a line of its own
+// k_serve6's 64 per-group-slot epoch words (bank = epoch & 1)
 #define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 64)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
@@ -113,7 +113,7 @@ struct ServeArgs {
                        // of two consecutive banks (the launch picks one by *epoch)
   int* err;            // host-visible (pinned) error word: 1 = a bounded spin ran out, 2 = a placement
                        // the launch was not sized for
-  unsigned* epoch;     // k_serve6: epoch (high 16 bits) | arrivals of the running launch (low 16 bits)
+  unsigned* epoch;     // k_serve6: per group slot (<= 64) its epoch word (bank = epoch & 1)
   int delay, delay_xcc;  // k_serve6 test hook (P3D_SERVE_TEST_DELAY): the workgroups on XCD delay_xcc start late
   int census_extra;    // test hook: k_serve5's census waits for this many workgroups beyond the grid; k_serve6 takes it as a placement failure
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)

@@ -12,8 +12,9 @@
 // on the critical path and 4 phases, instead of 32 tiles and 8 phases.
 //
 // One launch per call: the sync words alternate between two banks picked on the device (the
-// launch reads an epoch word, uses bank epoch & 1, zeroes the other for the next launch; the last
-// workgroup to arrive advances the epoch, so all of a launch's workgroups read the same one),
+// launch's groups each read their epoch word, use bank epoch & 1, zero their flags of the other for
+// the next launch; each group's rank-0 member advances the group's word at its end, when every
+// member has provably read it),
 // so a launch needs no memset in front and captured graphs replay correctly.  The epilogue
 // constants come from a table k_serve_prep forms per parameter version.
 //
@@ -145,17 +146,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // test hook (P3D_SERVE_TEST_DELAY): every workgroup of one XCD arrives ~delay x 3.4 us late
     if (p.delay > 0 && xcc == p.delay_xcc)
       for (int i = 0; i < p.delay; ++i) __builtin_amdgcn_s_sleep(127);
-    // arrival word: high 16 bits the launch epoch, low 16 bits this launch's arrivals so far.  The
-    // last workgroup to arrive resets the count and advances the epoch, so every workgroup of a
-    // launch reads the same epoch however late it starts, and the next launch (stream order: after
-    // this one completed) the next one.  (Round 3 advanced the epoch at the END of workgroup 0's
-    // work: a whole XCD group dispatched after workgroup 0 had finished read the advanced epoch,
-    // ran on the other bank and left its flags there for the next launch.)  One returning atomic
-    // per workgroup, in flight with the prologue's operand requests like the epoch read it replaces.
-    const unsigned v = __hip_atomic_fetch_add(p.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ep = v >> 16;
-    if ((v & 0xFFFFu) == gridDim.x - 1u)
-      __hip_atomic_fetch_add(p.epoch, 0x10000u - gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool bad = (gridDim.x & 7u) != 0u || S < 1 || S > 8 || p.census_extra;
     sh[0] = (int)(((unsigned)xcc - blockIdx.x) & 7u);   // (trace: the launch's starting XCD)
     sh[2] = bad ? 1 : 0;
@@ -215,8 +205,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     wq = tid < nl_ec ? p.ecg[(int64_t)nl_ec * T * 48 + tid] : 1.f;
   };
-  int r, n, gid, gi, ng;
-  place([&](int) { return nxg; }, xcc, rx, r, n, gid, gi, ng);
+  int r = 0, n = 1, gid = 0, gi = -1, ng = 0;
+  const bool placeable = (gridDim.x & 7u) == 0u && S >= 1 && S <= 8;
+  if (placeable) place([&](int) { return nxg; }, xcc, rx, r, n, gid, gi, ng);
+  // The group's epoch word (one per group slot; bank = epoch & 1).  Every member reads it at its
+  // start; the group's rank-0 member advances it at the END of its work, by which time every
+  // member has read it: rank 0's four waves read the whole K of every hidden layer, i.e. waited
+  // for a flag of every member of the group, which each posted after its read.  A late member --
+  // or a whole group dispatched late -- reads the epoch its own group is on.  (Round 3 kept one
+  // word for the launch, advanced by workgroup 0 at its end: a whole group dispatched after
+  // workgroup 0 had finished -- an idle one at max_groups = 1 -- read the advanced epoch, ran on the
+  // other bank and left its flags there for the next launch; one launch-wide arrival counter
+  // instead cost 2-3 us per launch: 256 returning atomics on one word, serialised.)
+  if (tid == 0 && placeable) ep = __hip_atomic_load(p.epoch + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the first unit's input-layer operands and the epilogue constants in flight with the epoch read
   prefetch(gi, (T * r) / n, (T * (r + 1)) / n);
   if (tid == 0) sh[3] = (int)(ep & 1u);
@@ -231,10 +232,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
   unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
-  {
-    unsigned* other = p.sync + (bank ^ 1) * P3D_SERVE_SYNC_WORDS;
-    for (int i = P3D_SERVE_FLAG0 + blockIdx.x * 256 + tid; i < P3D_SERVE_SYNC_WORDS; i += gridDim.x * 256) other[i] = 0u;
-  }
+  // the group's flags in the other bank, zeroed for the group's next launch (every member the same
+  // 64 words; nothing of this launch uses that bank).  Invariant: at the start of a launch the bank
+  // of a group slot's epoch holds zeros (an idle group posts nothing and does not advance).
+  if (placeable && tid < 64) p.sync[(bank ^ 1) * P3D_SERVE_SYNC_WORDS + P3D_SERVE_FLAG0 + 64 * gid + tid] = 0u;
   if (sh[2]) {
     // a placement this launch cannot use: no row of it is computed by this workgroup; it fills
     // a stripe of the output with NaN, so a caller who skips p3d_serve_check / p3d_error_flags
@@ -652,5 +653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
   }
+  if (r == 0 && tid == 0 && gi < p.nb)   // (every member has read the epoch by now: see its read)
+    __hip_atomic_fetch_add(p.epoch + gid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
