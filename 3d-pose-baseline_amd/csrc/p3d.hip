@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64 * WK) void k_fwd(FwdArgs p) {
     for (int s = 0; s < RS; ++s)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mt; sq += d * d; }
+        if (m0 + 16 * s + 4 * q + r < p.M) { const float d = z[s][r] - mt; sq = __builtin_fmaf(d, d, sq); }
     sq = p3d_colsum16(sq);
     if (p.bn == 4) {
       const int R = tgy;
@@ -849,8 +849,7 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
   float rstd = 1.f, inv = 1.f, shift = 0.f;
   if (p.bn) {
     rstd = 1.0f / sqrtf(var + p.eps);
-    inv = rstd * gam;
-    shift = bet - mean * inv;
+    p3d_bn_affine(mean, var, p.eps, gam, bet, inv, shift);   // (1 / sqrt(var + eps)) * gamma, as rstd * gamma
   }
   float xh[RS][4];
   float sg = 0.f, sgx = 0.f;
@@ -867,14 +866,14 @@ __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by,
       const bool ok = row < p.M;
       float gg = g[s][r];
       if (p.keep < 1.0f) gg = (gg * p3d_dropout_mask(p.keep, uu[s][r])) / p.keep;
-      const float a = p.bn ? zz[s][r] * inv + shift : zz[s][r];
+      const float a = p.bn ? p3d_bn_y(zz[s][r], inv, shift) : zz[s][r];   // the forward's own rounding
       if (p.relu && !(a > 0.0f)) gg = 0.0f;
       if (!ok) gg = 0.0f;
       g[s][r] = gg;
       const float x = (zz[s][r] - mean) * rstd;
       xh[s][r] = x;
       sg += gg;
-      sgx += gg * x;
+      sgx = __builtin_fmaf(gg, x, sgx);
     }
   if (p.bn) {
     sg = p3d_colsum16(sg);
@@ -949,6 +948,8 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   }
   p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, blockIdx.x, blockIdx.y, gridDim.y);
 }
+
+#include "p3d_ks.h"
 
 // =====================================================================================
 // BN-train backward, second half (split form): dz = inv/M * (M g - sum g - xhat sum g*xhat)
@@ -1582,6 +1583,9 @@ struct p3d_model {
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
                               // 128-B line each), then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
   int64_t xslots_off = 0;     // word offset of the slot arrays in xsync
+  int train_ks = 1;           // BN-train hidden layers with K split over 8 sibling workgroups (p3d_ks.h; env P3D_TRAIN_KS)
+  unsigned* kssync = nullptr; // K-split form: per site the column pairs' epoch words, then the sc1 and plain slot copies
+  int64_t ks_site_words = 0;
   int xchg_delay = 0;         // test hook: late row-tile siblings (env P3D_XCHG_TEST_DELAY, p3d_xchg.h)
   int xchg_remap = 1;         // exchange launches as 1-D grids with the siblings on one XCD (env P3D_XCHG_REMAP)
   // error words the kernels write and the host reads without a device round trip (pinned, mapped):
@@ -1761,6 +1765,7 @@ void free_all(p3d_model* m) {
   if (m->bf16s_part) (void)hipFree(m->bf16s_part);
   if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
+  if (m->kssync) (void)hipFree(m->kssync);
   if (m->errw) (void)hipHostFree(m->errw);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
   for (hipEvent_t e : m->sev) (void)hipEventDestroy(e);
@@ -2001,6 +2006,10 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_IN_TRAIN_WK")) m->in_train_wk = atoi(ev);
   if (const char* ev = getenv("P3D_DGRAD_OUT_WK")) m->dgrad_out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_XCHG_WK")) m->xchg_wk = atoi(ev);
+  if (const char* ev = getenv("P3D_TRAIN_KS")) m->train_ks = atoi(ev);
+  // the K-split form sums the 8-wave data gradient's partials: every form of the hidden data
+  // gradient then runs the 8-wave association, so all forms keep giving the same bits
+  if (m->train_ks) m->dgrad_wk = 8;
   if (const char* ev = getenv("P3D_DGRAD_WK")) m->dgrad_wk = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
   {
@@ -2012,6 +2021,15 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     const int64_t nx = m->xslots_off + (int64_t)2 * 2 * nl * P3D_XCHG_MAXR * L * 4;   // sc1 + plain copies
     if ((e = hipMalloc(&m->xsync, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->xsync, 0, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    if (m->train_ks && L % 256 == 0 && c.dtype == P3D_DTYPE_F32) {
+      // per site (layer, direction): L/32 epoch words (128 B apart), then 2 copies of
+      // [L/32][8][8][4][16][2] 16-B granules (L = 1024: 4 MB per copy)
+      const int64_t ncp = L / 32, gran = ncp * 8 * 8 * 4 * 16 * 2;
+      m->ks_site_words = ncp * P3D_XCHG_EPOCH_STRIDE + 2 * gran * 4;
+      const int64_t nk = (int64_t)2 * nl * m->ks_site_words;
+      if ((e = hipMalloc(&m->kssync, nk * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+      if ((e = hipMemset(m->kssync, 0, nk * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    }
     if ((e = hipHostMalloc((void**)&m->errw, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
       return cleanup(e);
     memset(m->errw, 0, 64 * sizeof(int));
@@ -2298,10 +2316,36 @@ static XchgSite xchg_site(const p3d_model* m, int slot) {
   return x;
 }
 
+// K-split BN-train form (p3d_ks.h): hidden layers at B <= 64 whose column pairs' 8 sibling
+// workgroups all fit on the device at once.  out_w = the produced width (N of the forward, K of the
+// data gradient), k = the contraction.
+static bool use_ks(const p3d_model* m, int k, int out_w, int M) {
+  return m->train_ks && m->kssync && m->train_xchg && M <= 64 && out_w % 256 == 0 && out_w <= m->cfg.linear_size &&
+         k % 128 == 0 && 8 * (out_w / 32) <= m->num_cus;
+}
+static KsSite ks_site(const p3d_model* m, int slot) {
+  const int64_t ncp = m->cfg.linear_size / 32;
+  KsSite k;
+  unsigned* base = m->kssync + (int64_t)slot * m->ks_site_words;
+  const int64_t gran = ncp * 8 * 8 * 4 * 16 * 2;
+  k.epoch = base;
+  k.slots = (float*)(base + ncp * P3D_XCHG_EPOCH_STRIDE);
+  k.near = k.slots + gran * 4;
+  k.err = m->xerr;
+  return k;
+}
+
 static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
   FwdArgs a = a0;
   a.bn = 3; a.bnpart = m->bnpart;
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
+  if (kind == 1 && use_ks(m, a.K, a.N, a.M)) {   // one launch, K split over 8 sibling workgroups
+    a.bn = 4;
+    ProfScope ps(m, "fwd_hidden_train_ks");
+    go(ps, k_fwd_ks<8>, dim3((unsigned)(8 * (a.N / 32))), dim3(512), st, a, ks_site(m, a.site));
+    LAUNCH_CHECK("k_fwd_ks");
+    return P3D_OK;
+  }
   if (use_xchg(m, a.N, a.M)) {   // BN-train layer as ONE launch
     a.bn = 4; a.xs = xchg_site(m, a.site);
     static const char* tags[2] = {"fwd_in_train_x", "fwd_hidden_train_x"};
@@ -3236,6 +3280,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           const int gx = (int)grid.x, gy = (int)grid.y;
           go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, dim3((unsigned)(gx * gy + mw.begin[mw.n])), dim3(512), st, a, mw,
              gx, gy);
+        } else if (dz_pk && xchg && use_ks(m, ly.N, a.K, a.M)) {
+          go(ps, k_dgrad_ks<8>, dim3((unsigned)(8 * (a.K / 32))), dim3(512), st, a, ks_site(m, nl + l - 1));
         } else if (dz_pk) {
           dim3 g = grid;
           if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }

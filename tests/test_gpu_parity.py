@@ -228,26 +228,37 @@ def test_train_steps_track_oracle(split, xchg, monkeypatch):
 @pytest.mark.parametrize("L,B,keep,delay", [(1024, 64, 0.5, 0), (256, 17, 0.5, 0), (256, 64, 1.0, 0),
                                            (256, 200, 0.5, 0), (1024, 64, 0.5, 8), (256, 200, 0.5, 8)])
 def test_bn_exchange_bit_identical_to_split(L, B, keep, delay, monkeypatch):
-    """BN-train layers as ONE launch (row-tile workgroups swap their column statistics in the
-    launch, p3d_xchg.h) == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit, over 4
-    fused train steps: outputs, loss, weights, Adam slots, moving statistics.  B = 200 (13 row
-    tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4.
+    """BN-train layers as ONE launch == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit,
+    over 4 fused train steps: outputs, loss, weights, Adam slots, moving statistics.  Two one-launch
+    forms: the K-split form (p3d_ks.h, round 4: 8 sibling workgroups of a column pair each contract
+    one eighth of K for all rows and swap partial products; B <= 64) and the row-tile exchange form
+    (p3d_xchg.h: row-tile workgroups swap column moments; B = 200 there too).  All three run the
+    8-wave association of the hidden data gradient (P3D_DGRAD_WK=8, the K-split form's).  B = 200
+    (13 row tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4.
     delay > 0 (test hook P3D_XCHG_TEST_DELAY): the last row-tile workgroup of every odd column
-    tile sleeps ~27 us before it reads its tag, so other column tiles finish their swaps (and
-    advance their epochs) first -- with one epoch word per site that late sibling read a tag
-    its siblings did not hold (advisor r2); with the column tile's own word it must not matter."""
+    tile of the exchange form sleeps ~27 us before it reads its tag, so other column tiles finish
+    their swaps (and advance their epochs) first -- with one epoch word per site that late
+    sibling read a tag its siblings did not hold (advisor r2); with the column tile's own word it
+    must not matter."""
     import ctypes
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=2, residual=True, batch_norm=True)
     st = ref_mlp.init_state(cfg, seed=6, bn_seed=7)
+    forms = (("ks", {"P3D_TRAIN_XCHG": "1", "P3D_TRAIN_KS": "1"}),
+             ("x", {"P3D_TRAIN_XCHG": "1", "P3D_TRAIN_KS": "0", "P3D_DGRAD_WK": "8", "P3D_XCHG_TEST_DELAY": str(delay)}),
+             ("split", {"P3D_TRAIN_XCHG": "0", "P3D_TRAIN_KS": "1"}))
     ms = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("P3D_TRAIN_XCHG", flag)
-        monkeypatch.setenv("P3D_XCHG_TEST_DELAY", str(delay if flag == "1" else 0))
+    for _, env in forms:
+        for k in ("P3D_TRAIN_XCHG", "P3D_TRAIN_KS", "P3D_DGRAD_WK", "P3D_XCHG_TEST_DELAY"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         m = linear_model.LinearModel(L, 2, True, True, False, B, 1e-3, "/tmp/p3d_test", seed=9, max_batch=max(B, 64))
         m.set_weights({**st.params, **st.moving})
         ms.append(m)
-    xm, sm = ms
+    for k in ("P3D_TRAIN_XCHG", "P3D_TRAIN_KS", "P3D_DGRAD_WK", "P3D_XCHG_TEST_DELAY"):
+        monkeypatch.delenv(k, raising=False)
+    km, xm, sm = ms
     rng = np.random.default_rng(L + B)
     for step in range(4):
         x = torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)).cuda()
@@ -261,19 +272,24 @@ def test_bn_exchange_bit_identical_to_split(L, B, keep, delay, monkeypatch):
                 buf = ctypes.create_string_buffer(1 << 14)
                 _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
                 m.tags = {ln.split("\t")[0] for ln in buf.value.decode().strip().splitlines()}
-        assert torch.equal(ys[0], ys[1]), step
-        assert torch.equal(xm._loss_dev, sm._loss_dev), step
-    xm.sync_check()
-    xm.check_errors()
+        for (tag, _), y in zip(forms[1:], ys[1:]):
+            assert torch.equal(ys[0], y), (step, tag)
+        assert torch.equal(km._loss_dev, xm._loss_dev) and torch.equal(km._loss_dev, sm._loss_dev), step
+    for m in (km, xm):
+        m.sync_check()
+        m.check_errors()
     for k in ("params", "moving", "adam_m", "adam_v"):
-        if xm.flat[k] is not None:
-            assert torch.equal(xm.flat[k], sm.flat[k]), k
-    assert xm.get_step() == sm.get_step()
-    # the exchange form really ran: no second BN launch in either direction
-    assert "fwd_hidden_train_x" in xm.tags and not {"bn_fwd", "bn_bwd"} & xm.tags, xm.tags
+        if km.flat[k] is not None:
+            assert torch.equal(km.flat[k], xm.flat[k]), k
+            assert torch.equal(km.flat[k], sm.flat[k]), k
+    assert km.get_step() == xm.get_step() == sm.get_step()
+    # the one-launch forms really ran: no second BN launch in either direction
+    want_ks = B <= 64 and L % 256 == 0
+    assert ("fwd_hidden_train_ks" in km.tags) == want_ks, km.tags
+    assert "fwd_hidden_train_x" in xm.tags and not {"bn_fwd", "bn_bwd"} & (xm.tags | km.tags), (xm.tags, km.tags)
     assert {"bn_fwd", "bn_bwd"} <= sm.tags, sm.tags
-    xm.close()
-    sm.close()
+    for m in ms:
+        m.close()
 
 
 @pytest.mark.parametrize("B", [128, 200])
