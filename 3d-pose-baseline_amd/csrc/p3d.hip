@@ -949,7 +949,6 @@ __global__ __launch_bounds__(64 * WK) void k_dgrad(BwdArgs p) {
   p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
-#include "p3d_ks.h"
 
 // =====================================================================================
 // BN-train backward, second half (split form): dz = inv/M * (M g - sum g - xhat sum g*xhat)
@@ -1063,6 +1062,14 @@ __device__ __forceinline__ void p3d_stage64_load(Stage64& st, const float* __res
     }
   }
 }
+// LDS image of a staged 64 x 64 chunk.  SW = false: rows WG_LDS_STRIDE floats apart; SW = true:
+// rows 64 floats apart (16 KB per operand), column c of row r at c ^ (16 (r & 3)) -- the four
+// row phases of a wave's MFMA operand reads land in four different 16-bank quarters.
+template <bool SW>
+__device__ __forceinline__ int p3d_wg_lidx(int r, int c) {
+  return SW ? r * 64 + (c ^ ((r & 3) << 4)) : r * WG_LDS_STRIDE + c;
+}
+template <bool SW = false>
 __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const Stage64& st, int pk) {
   const int tid = threadIdx.x;
   if (pk) {
@@ -1072,14 +1079,14 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
       const int rt = chunk >> 2, gg = chunk & 3;
       const int row = 16 * rt + (ln & 15), col = 16 * gg + 4 * (ln >> 4);
       const bool ok = (st.ok >> e) & 1u;
-      *(f32x4*)&dst[row * WG_LDS_STRIDE + col] =
+      *(f32x4*)&dst[p3d_wg_lidx<SW>(row, col)] =
           ok ? f32x4{st.f[4 * e], st.f[4 * e + 1], st.f[4 * e + 2], st.f[4 * e + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = tid + 256 * k, m = e >> 6, c = e & 63;
-      dst[m * WG_LDS_STRIDE + c] = ((st.ok >> k) & 1u) ? st.f[k] : 0.f;
+      dst[p3d_wg_lidx<SW>(m, c)] = ((st.ok >> k) & 1u) ? st.f[k] : 0.f;
     }
   }
 }
@@ -1093,56 +1100,69 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
 #else
 #define P3D_WG_STAMP(k) do { } while (0)
 #endif
+// NOADAM: the gradient-only form (data-parallel steps, whose optimizer runs behind the
+// all-reduce): no optimizer code, swizzled 16 KB operand images and db's partials in the X image
+// once it is consumed -- 32 KB of LDS and <= 96 registers, so 5 workgroups fit on a CU and the
+// 1,056 tiles of cfg3 run in ONE round (the general form's 41 KB / 131 registers hold 3 per CU:
+// 768 + 288 tiles in two rounds).  The same arithmetic: the same bits.
+template <bool NOADAM = false>
 __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
   P3D_WG_STAMP(0);
-  __shared__ __attribute__((aligned(16))) float xs[64 * WG_LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) float zs[64 * WG_LDS_STRIDE];
+  constexpr int XS = NOADAM ? 64 * 64 : 64 * WG_LDS_STRIDE;
+  __shared__ __attribute__((aligned(16))) float xs[XS];
+  __shared__ __attribute__((aligned(16))) float zs[XS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
   const int n0 = bx * 64, k0 = by * 64;
   f32x4 acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __shared__ float dbp[4][64];
+  __shared__ float dbp_own[NOADAM ? 1 : 4][64];
+  float (*dbp)[64] = NOADAM ? reinterpret_cast<float (*)[64]>(xs) : dbp_own;
   const bool do_db = p.db && by == 0;
   float dbs = 0.f;   // wave w: rows 16w .. 16w+15 of column `lane` (summed in row order)
   // the step's alpha, requested before the contraction (its latency hides there)
-  const float alpha_pre = (p.adam && p.alpha_dev) ? *p.alpha_dev : 0.f;
+  const float alpha_pre = (!NOADAM && p.adam && p.alpha_dev) ? *p.alpha_dev : 0.f;
   for (int mc = 0; mc < p.M; mc += 64) {
     Stage64 sx, sz;
     p3d_stage64_load(sx, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
     p3d_stage64_load(sz, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
-    p3d_stage64_store(xs, sx, p.xpk);
-    p3d_stage64_store(zs, sz, p.zpk);
+    p3d_stage64_store<NOADAM>(xs, sx, p.xpk);
+    p3d_stage64_store<NOADAM>(zs, sz, p.zpk);
     __syncthreads();
     P3D_WG_STAMP(1);
-#pragma unroll 4
+#pragma unroll NOADAM ? 2 : 4
     for (int t = 0; t < 16; ++t) {
       const int m = 4 * t + q;
-      const float a = xs[m * WG_LDS_STRIDE + 16 * w + i];
+      const float a = xs[p3d_wg_lidx<NOADAM>(m, 16 * w + i)];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[m * WG_LDS_STRIDE + 16 * s + i], acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[p3d_wg_lidx<NOADAM>(m, 16 * s + i)], acc[s], 0, 0, 0);
     }
     if (do_db) {
-      float v[16];
+      if (NOADAM) {   // (the same sums, fewer registers live)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = zs[(16 * w + r) * WG_LDS_STRIDE + lane];
+        for (int r = 0; r < 16; ++r) dbs += zs[p3d_wg_lidx<NOADAM>(16 * w + r, lane)];
+      } else {
+        float v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dbs += v[r];
+        for (int r = 0; r < 16; ++r) v[r] = zs[p3d_wg_lidx<NOADAM>(16 * w + r, lane)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dbs += v[r];
+      }
     }
     __syncthreads();
   }
   P3D_WG_STAMP(2);
   float alpha = 0.f;
-  if (p.adam)
+  if (!NOADAM && p.adam)
     alpha = p.alpha_dev ? alpha_pre : p3d_adam_alpha(p.af.st, p.af.lr_host, p.af.lr0, p.af.decay_steps, p.af.decay_rate);
   if (do_db) {
     dbp[w][lane] = dbs;
     __syncthreads();
     if (w == 0 && n0 + lane < p.N) {
       const float gb = ((dbp[0][lane] + dbp[1][lane]) + dbp[2][lane]) + dbp[3][lane];
-      if (p.adam) {
+      if (!NOADAM && p.adam) {
         p.db[n0 + lane] = gb;   // the bias gradient stays visible in the grads buffer
         const int64_t o = p.boff + n0 + lane;
         float ww = p.w[o], mm = p.m[o], vv = p.v[o];
@@ -1153,7 +1173,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
       }
     }
   }
-  if (p.adam && p.bn_adam && bx == 0 && tid < 64 && k0 + tid < p.K) {
+  if (!NOADAM && p.adam && p.bn_adam && bx == 0 && tid < 64 && k0 + tid < p.K) {
     const float omb1 = 1.0f - p.af.b1, omb2 = 1.0f - p.af.b2;
     const int64_t og = p.goff + k0 + tid, ob = p.btoff + k0 + tid;
     float w1 = p.w[og], m1 = p.m[og], v1 = p.v[og];
@@ -1163,7 +1183,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     p3d_adam1(w2, m2, v2, p.gflat[ob], alpha, omb1, omb2, p.af.eps);
     p.w[ob] = w2; p.m[ob] = m2; p.v[ob] = v2;
   }
-  if (p.adam) {
+  if (!NOADAM && p.adam) {
     // gradient tile -> LDS (reusing the staging buffer), then Adam + re-pack of W's tile
     float (*tile)[65] = reinterpret_cast<float (*)[65]>(xs);
 #pragma unroll
@@ -1213,25 +1233,46 @@ struct WgradMulti {
   StepState* advance;            // if set: this launch's workgroup 0 advances the step state at its end
   WgradLayer ly[P3D_WG_MULTI];
 };
+template <bool NOADAM = false>
 __device__ __forceinline__ void p3d_wgrad_multi_tile(const WgradMulti& mw, int b) {
   P3D_WG_STAMP(4);
   int j = 0;
+  WgradArgs p{};
+  int beg = 0, gx = 1;
+  if (NOADAM) {
+    // constant indices only (a runtime index into the argument block made the compiler copy it
+    // to scratch at the 96-register budget)
+#pragma unroll
+    for (int k = 1; k < P3D_WG_MULTI; ++k)
+      if (k < mw.n && b >= mw.begin[k]) j = k;
+#pragma unroll
+    for (int k = 0; k < P3D_WG_MULTI; ++k)
+      if (k == j) {
+        const WgradLayer& l = mw.ly[k];
+        p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
+        p.M = l.M; p.K = l.K; p.N = l.N; p.dW = l.dW; p.db = l.db;
+        beg = mw.begin[k]; gx = mw.gx[k];
+      }
+    const int loc = b - beg;
+    p3d_wgrad_tile<NOADAM>(p, loc % gx, loc / gx);
+    return;
+  }
   while (j + 1 < mw.n && b >= mw.begin[j + 1]) ++j;
   const WgradLayer& l = mw.ly[j];
-  WgradArgs p{};
   p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
   p.M = l.M; p.K = l.K; p.N = l.N; p.dW = l.dW; p.db = l.db;
-  if (mw.adam) {
+  if (!NOADAM && mw.adam) {
     p.adam = 1; p.af = mw.af; p.w = mw.w; p.m = mw.m; p.v = mw.v; p.woff = l.woff; p.boff = l.boff;
     p.wd = l.wd; p.wf = l.wf;
     p.bn_adam = l.bn_adam; p.gflat = mw.gflat; p.goff = l.goff; p.btoff = l.btoff;
     p.alpha_dev = mw.alpha_dev;
   }
   const int loc = b - mw.begin[j];
-  p3d_wgrad_tile(p, loc % mw.gx[j], loc / mw.gx[j]);
+  p3d_wgrad_tile<NOADAM>(p, loc % mw.gx[j], loc / mw.gx[j]);
 }
-__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
-  p3d_wgrad_multi_tile(mw, blockIdx.x);
+template <bool NOADAM>
+__device__ __forceinline__ void p3d_wgrad_multi_body(const WgradMulti& mw) {
+  p3d_wgrad_multi_tile<NOADAM>(mw, blockIdx.x);
   // the step's last launch: nothing in it reads the step state (alpha came from alpha_dev),
   // so one thread may advance it here instead of a k_step_advance launch
   if (mw.advance && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1241,6 +1282,9 @@ __global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) {
     st->global_step = st->global_step + 1;
   }
 }
+__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
+// the gradient-only form, 5 workgroups (5 waves per SIMD) per CU
+__global__ __launch_bounds__(256, 4) void k_wgrad_grad(WgradMulti mw) { p3d_wgrad_multi_body<true>(mw); }
 
 // A data-gradient launch carrying the weight-gradient (+ fused Adam) tiles of the layer above:
 // blocks [0, gx*gy) are k_dgrad's tiles of this layer, the rest mw's tiles (256 threads: the
@@ -1583,9 +1627,6 @@ struct p3d_model {
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
                               // 128-B line each), then per site P3D_XCHG_MAXR x L 16-B slots (p3d_xchg.h)
   int64_t xslots_off = 0;     // word offset of the slot arrays in xsync
-  int train_ks = 1;           // BN-train hidden layers with K split over 8 sibling workgroups (p3d_ks.h; env P3D_TRAIN_KS)
-  unsigned* kssync = nullptr; // K-split form: per site the column pairs' epoch words, then the sc1 and plain slot copies
-  int64_t ks_site_words = 0;
   int xchg_delay = 0;         // test hook: late row-tile siblings (env P3D_XCHG_TEST_DELAY, p3d_xchg.h)
   int xchg_remap = 1;         // exchange launches as 1-D grids with the siblings on one XCD (env P3D_XCHG_REMAP)
   // error words the kernels write and the host reads without a device round trip (pinned, mapped):
@@ -1649,6 +1690,14 @@ struct p3d_model {
   int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
   int gemv_maxb = 4;        // inference at B <= gemv_maxb runs the k_gemv layers (env P3D_GEMV_MAXB, 0..4)
+  int gemv_fold = 1;        // ... with the input / output layers folded into the first / last hidden layer's
+                            // launch (k_gemv_fold; env P3D_GEMV_FOLD; the same bits either way)
+  int gemv_chain = 0;       // ... as ONE persistent launch where the hidden layers' tiles fit on the device
+                            // (k_gemv_chain; env P3D_GEMV_CHAIN=1, opt-in until validated on the box; the same bits)
+  int gemv_slots = 0;       // workspace slots (ws_row / 16) the fold's hand-off buffer covers (others unfolded)
+  int64_t gemv_slot_floats = 0;     // hand-off floats per slot (the chain's H layers, or the fold's one)
+  float* gemv_hand = nullptr;       // [slot][layers][4 rows][L / 2] 16-B granules (layer-output hand-offs)
+  unsigned* gemv_epoch = nullptr;   // [slot] epoch words, P3D_XCHG_EPOCH_STRIDE apart
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
@@ -1765,7 +1814,8 @@ void free_all(p3d_model* m) {
   if (m->bf16s_part) (void)hipFree(m->bf16s_part);
   if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
-  if (m->kssync) (void)hipFree(m->kssync);
+  if (m->gemv_hand) (void)hipFree(m->gemv_hand);
+  if (m->gemv_epoch) (void)hipFree(m->gemv_epoch);
   if (m->errw) (void)hipHostFree(m->errw);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
   for (hipEvent_t e : m->sev) (void)hipEventDestroy(e);
@@ -2001,15 +2051,13 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_OUT_BIG")) m->out_big = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
+  if (const char* ev = getenv("P3D_GEMV_FOLD")) m->gemv_fold = atoi(ev);
+  if (const char* ev = getenv("P3D_GEMV_CHAIN")) m->gemv_chain = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_IN_TRAIN_WK")) m->in_train_wk = atoi(ev);
   if (const char* ev = getenv("P3D_DGRAD_OUT_WK")) m->dgrad_out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_XCHG_WK")) m->xchg_wk = atoi(ev);
-  if (const char* ev = getenv("P3D_TRAIN_KS")) m->train_ks = atoi(ev);
-  // the K-split form sums the 8-wave data gradient's partials: every form of the hidden data
-  // gradient then runs the 8-wave association, so all forms keep giving the same bits
-  if (m->train_ks) m->dgrad_wk = 8;
   if (const char* ev = getenv("P3D_DGRAD_WK")) m->dgrad_wk = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
   {
@@ -2021,14 +2069,19 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     const int64_t nx = m->xslots_off + (int64_t)2 * 2 * nl * P3D_XCHG_MAXR * L * 4;   // sc1 + plain copies
     if ((e = hipMalloc(&m->xsync, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->xsync, 0, nx * sizeof(unsigned))) != hipSuccess) return cleanup(e);
-    if (m->train_ks && L % 256 == 0 && c.dtype == P3D_DTYPE_F32) {
-      // per site (layer, direction): L/32 epoch words (128 B apart), then 2 copies of
-      // [L/32][8][8][4][16][2] 16-B granules (L = 1024: 4 MB per copy)
-      const int64_t ncp = L / 32, gran = ncp * 8 * 8 * 4 * 16 * 2;
-      m->ks_site_words = ncp * P3D_XCHG_EPOCH_STRIDE + 2 * gran * 4;
-      const int64_t nk = (int64_t)2 * nl * m->ks_site_words;
-      if ((e = hipMalloc(&m->kssync, nk * sizeof(unsigned))) != hipSuccess) return cleanup(e);
-      if ((e = hipMemset(m->kssync, 0, nk * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    if (m->gemv_fold && m->gemv_maxb > 0 && c.dtype == P3D_DTYPE_F32 && L <= P3D_GEMV_FOLD_MAXK) {
+      // batch <= 4 fold: the first 64 workspace slots (ws_row < 1024) get a hand-off area of
+      // 4 rows x L / 2 granules (32 KB at L = 1024) and an epoch word each
+      m->gemv_slots = (int)std::min<int64_t>(64, (c.max_batch + 15) / 16);
+      const int H = nl - 2;
+      const bool chain = H >= 1 && H <= P3D_GEMV_CHAIN_MAXH && L <= P3D_GEMV_CHAIN_MAXK && H * (L / 16) <= m->num_cus;
+      m->gemv_slot_floats = (int64_t)(chain ? H : 1) * 4 * (L / 2) * 4;
+      const int64_t nh = (int64_t)m->gemv_slots * m->gemv_slot_floats;
+      if ((e = hipMalloc(&m->gemv_hand, nh * sizeof(float))) != hipSuccess) return cleanup(e);
+      if ((e = hipMemset(m->gemv_hand, 0, nh * sizeof(float))) != hipSuccess) return cleanup(e);
+      const int64_t ne = (int64_t)m->gemv_slots * P3D_XCHG_EPOCH_STRIDE;
+      if ((e = hipMalloc(&m->gemv_epoch, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+      if ((e = hipMemset(m->gemv_epoch, 0, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
     }
     if ((e = hipHostMalloc((void**)&m->errw, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
       return cleanup(e);
@@ -2316,36 +2369,10 @@ static XchgSite xchg_site(const p3d_model* m, int slot) {
   return x;
 }
 
-// K-split BN-train form (p3d_ks.h): hidden layers at B <= 64 whose column pairs' 8 sibling
-// workgroups all fit on the device at once.  out_w = the produced width (N of the forward, K of the
-// data gradient), k = the contraction.
-static bool use_ks(const p3d_model* m, int k, int out_w, int M) {
-  return m->train_ks && m->kssync && m->train_xchg && M <= 64 && out_w % 256 == 0 && out_w <= m->cfg.linear_size &&
-         k % 128 == 0 && 8 * (out_w / 32) <= m->num_cus;
-}
-static KsSite ks_site(const p3d_model* m, int slot) {
-  const int64_t ncp = m->cfg.linear_size / 32;
-  KsSite k;
-  unsigned* base = m->kssync + (int64_t)slot * m->ks_site_words;
-  const int64_t gran = ncp * 8 * 8 * 4 * 16 * 2;
-  k.epoch = base;
-  k.slots = (float*)(base + ncp * P3D_XCHG_EPOCH_STRIDE);
-  k.near = k.slots + gran * 4;
-  k.err = m->xerr;
-  return k;
-}
-
 static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream_t st) {
   FwdArgs a = a0;
   a.bn = 3; a.bnpart = m->bnpart;
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
-  if (kind == 1 && use_ks(m, a.K, a.N, a.M)) {   // one launch, K split over 8 sibling workgroups
-    a.bn = 4;
-    ProfScope ps(m, "fwd_hidden_train_ks");
-    go(ps, k_fwd_ks<8>, dim3((unsigned)(8 * (a.N / 32))), dim3(512), st, a, ks_site(m, a.site));
-    LAUNCH_CHECK("k_fwd_ks");
-    return P3D_OK;
-  }
   if (use_xchg(m, a.N, a.M)) {   // BN-train layer as ONE launch
     a.bn = 4; a.xs = xchg_site(m, a.site);
     static const char* tags[2] = {"fwd_in_train_x", "fwd_hidden_train_x"};
@@ -2541,16 +2568,18 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
   return P3D_OK;
 }
 
-// Batch <= 4 inference (p3d_gemv.h): every layer as one weight-streaming k_gemv launch.
+// Batch <= 4 inference (p3d_gemv.h): every layer as one weight-streaming k_gemv launch, the input
+// and output layers folded into the first / last hidden layer's launch (k_gemv_fold) where the
+// workspace slot has a hand-off area -- four launches instead of six at num_layers = 2, same bits.
 static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float keep_prob, uint64_t seed,
-                        uint64_t ctr, int64_t row_offset, int64_t wsoff, hipStream_t st) {
+                        uint64_t ctr, int64_t row_offset, int64_t ws_row, hipStream_t st) {
   const p3d_cfg& c = m->cfg;
   const int nl = (int)m->layers.size();
-  const float* in = x;
-  for (int l = 0; l < nl; ++l) {
+  const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
+  auto fill = [&](int l, const float* in, GemvArgs& a) {
     const Layer& ly = m->layers[l];
     const bool last = (l == nl - 1);
-    GemvArgs a{};
+    a = GemvArgs{};
     a.X = in; a.ldx = c.input_size; a.xpk = l > 0;
     a.Wf = m->wpk + ly.wf;
     a.bias = m->flat[0] + ly.b;
@@ -2570,6 +2599,67 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
     if (c.residual && second) a.res = m->act[l - 2] + wsoff;
     if (last) { a.Y = y; a.ldy = ly.N; a.ypk = 0; }
     else { a.Y = m->act[l] + wsoff; a.ldy = 0; a.ypk = 1; }
+  };
+  const int64_t slot = ws_row >> 4;
+  const int L = c.linear_size;
+  const bool fold = m->gemv_fold && m->gemv_hand && slot < m->gemv_slots && nl >= 4 && L % 16 == 0 &&
+                    L <= P3D_GEMV_FOLD_MAXK && c.input_size == P3D_GEMV_FOLD_MAXIN &&
+                    c.output_size <= 64;
+  const int H = nl - 2, T = L / 16;
+  if (fold && m->gemv_chain && H <= P3D_GEMV_CHAIN_MAXH && L <= P3D_GEMV_CHAIN_MAXK && H * T <= m->num_cus &&
+      m->gemv_slot_floats >= (int64_t)H * 4 * (L / 2) * 4) {
+    GemvChain ch{};
+    fill(0, x, ch.in);
+    ch.in.Y = nullptr;
+    for (int l = 1; l <= H; ++l) {
+      fill(l, nullptr, ch.ly[l - 1]);
+      ch.ly[l - 1].res = nullptr;   // (added by the chain itself)
+      ch.ly[l - 1].Y = nullptr;
+    }
+    fill(nl - 1, nullptr, ch.out);
+    ch.H = H; ch.T = T; ch.res = c.residual ? 1 : 0;
+    ch.hand = m->gemv_hand + slot * m->gemv_slot_floats;
+    ch.epoch = m->gemv_epoch + slot * P3D_XCHG_EPOCH_STRIDE;
+    ch.err = m->xerr;
+    {
+      ProfScope ps(m, "gemv_chain");
+      go(ps, k_gemv_chain<4, 4>, dim3((unsigned)(H * T)), dim3(1024), st, ch);
+    }
+    LAUNCH_CHECK("k_gemv_chain");
+    return P3D_OK;
+  }
+  const float* in = x;
+  for (int l = 0; l < nl; ++l) {
+    const bool last = (l == nl - 1);
+    GemvArgs a;
+    fill(l, in, a);
+    if (fold && (l == 0 || l == nl - 1)) continue;   // run inside the first / last hidden layer's launch
+    if (fold && (l == 1 || l == nl - 2)) {
+      GemvFold f{};
+      if (l == 1) {
+        f.fin = 1;
+        fill(0, x, f.in);
+        // layer 0's output is read again only as layer 2's residual
+        if (!(c.residual && nl - 2 >= 2)) f.in.Y = nullptr;
+      }
+      if (l == nl - 2) {
+        f.fout = 1;
+        fill(nl - 1, nullptr, f.out);
+        f.hand = m->gemv_hand + slot * m->gemv_slot_floats;
+        f.epoch = m->gemv_epoch + slot * P3D_XCHG_EPOCH_STRIDE;
+        f.err = m->xerr;
+        a.Y = nullptr;
+      }
+      const dim3 grid((unsigned)(L / 16 + (f.fout ? 1 : 0)));
+      {
+        ProfScope ps(m, f.fin ? (f.fout ? "gemv_in_hidden_out" : "gemv_in_hidden") : "gemv_hidden_out");
+        go(ps, k_gemv_fold<4, 16, 4>, grid, dim3(1024), st, a, f);
+      }
+      LAUNCH_CHECK("k_gemv_fold");
+      in = m->act[l] + wsoff;
+      continue;
+    }
+    const Layer& ly = m->layers[l];
     const dim3 grid((unsigned)((ly.N + 15) / 16));
     {
       ProfScope ps(m, l == 0 ? "gemv_in" : (last ? "gemv_out" : "gemv_hidden"));
@@ -2628,7 +2718,7 @@ static int forward_impl(p3d_model* m, const float* x, int64_t B, float* y, int32
   const float decay = 1.0f - c.bn_momentum;
   const int nl = (int)m->layers.size();
   const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
-  if (!training && !tgt && B <= m->gemv_maxb) return forward_gemv(m, x, B, y, keep_prob, seed, ctr, row_offset, wsoff, st);
+  if (!training && !tgt && B <= m->gemv_maxb) return forward_gemv(m, x, B, y, keep_prob, seed, ctr, row_offset, ws_row, st);
   const float* in = x;
   for (int l = 0; l < nl; ++l) {
     const Layer& ly = m->layers[l];
@@ -3158,7 +3248,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     HIP_TRY(hipEventRecord(m->sev[l], st));
     HIP_TRY(hipStreamWaitEvent(m->side, m->sev[l], 0));
     ProfScope ps(m, "wgrad_side");
-    go(ps, k_wgrad_multi, dim3(one.begin[1]), dim3(256), m->side, one);
+    if (one.adam) go(ps, k_wgrad_multi, dim3(one.begin[1]), dim3(256), m->side, one);
+    else go(ps, k_wgrad_grad, dim3(one.begin[1]), dim3(256), m->side, one);
     LAUNCH_CHECK("k_wgrad_multi (side)");
     side_used = true;
     return P3D_OK;
@@ -3171,7 +3262,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
     aev_pending = (int)kb;
     if (mw.n > 0) {
       ProfScope ps(m, "wgrad_bucket");
-      go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+      if (mw.adam) go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+      else go(ps, k_wgrad_grad, dim3(mw.begin[mw.n]), dim3(256), st, mw);
       LAUNCH_CHECK("k_wgrad_multi (bucket)");
       mw.n = 0;
       mw.begin[0] = 0;
@@ -3280,8 +3372,6 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           const int gx = (int)grid.x, gy = (int)grid.y;
           go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, dim3((unsigned)(gx * gy + mw.begin[mw.n])), dim3(512), st, a, mw,
              gx, gy);
-        } else if (dz_pk && xchg && use_ks(m, ly.N, a.K, a.M)) {
-          go(ps, k_dgrad_ks<8>, dim3((unsigned)(8 * (a.K / 32))), dim3(512), st, a, ks_site(m, nl + l - 1));
         } else if (dz_pk) {
           dim3 g = grid;
           if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
@@ -3333,7 +3423,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
   if (multi && mw.n > 0) {
     if (fused_tail) { mw.advance = m->dstate; m->step_advanced = true; }   // the step's last launch
     ProfScope ps(m, side_used ? "wgrad_tail" : "wgrad_multi");
-    go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+    if (mw.adam) go(ps, k_wgrad_multi, dim3(mw.begin[mw.n]), dim3(256), st, mw);
+    else go(ps, k_wgrad_grad, dim3(mw.begin[mw.n]), dim3(256), st, mw);
     LAUNCH_CHECK("k_wgrad_multi");
   }
   if (!m->gev.empty() && !bucketed && !c.max_norm)   // (per-layer k_wgrad form: every bucket at the end)

@@ -18,12 +18,24 @@
 // dropout, residual).  The epilogue operands are requested at kernel start by the lanes that
 // use them.
 //
-// Why one launch per layer (not a persistent chain): the hand-off of a layer's 1024 features
-// from the 64 producing workgroups to every consumer costs ~3-4 us inside a launch (price list
-// rows allgather / barrier-xcd of MI355X_MICROARCH.md) against ~1.2 us for the dependent kernel
-// boundary between short GEMV kernels (row boundary).
+// Why not one persistent chain: the hand-off of a layer's 1024 features from the 64 producing
+// workgroups to EVERY consumer costs ~3-4 us inside a launch (price list rows allgather /
+// barrier-xcd of MI355X_MICROARCH.md) against ~1.2 us for the dependent kernel boundary between
+// short GEMV kernels (row boundary).  Two of the six launches are folded away all the same
+// (k_gemv_fold, round 4), where neither costs an all-to-all:
+//   * the input layer (K = 32, 128 KB of weights) is recomputed by every workgroup of the first
+//     hidden layer: 32 FMAs per feature and row, its weights read from the XCD's L2 beside the
+//     hidden layer's own slice; each workgroup writes its own 16 columns of the input layer's
+//     output for the residual of layer 2;
+//   * the output layer (48 x 1024) is run by ONE extra workgroup of the last hidden layer's launch:
+//     it requests its 192 KB of weights at kernel start, then gathers the 64 producers' outputs
+//     (a many-to-one hand-off, ~1 us, data-tagged granules as in p3d_xchg.h) and contracts them.
+// Both folds keep k_gemv's associations (input layer: the 2-wave split of k_gemv<4, 2, 4>; output
+// layer: the 16-wave split of k_gemv<4, 16, 4>), so the folded chain gives the unfolded chain's
+// bits (tests/test_gpu_parity.py::test_gemv_small_batch).
 #pragma once
 #include "p3d_kernels.h"
+#include "p3d_xchg.h"
 
 struct GemvArgs {
   const float* X; int64_t ldx; int xpk;   // X packed (hidden input) or row-major, leading dim ldx
@@ -40,6 +52,74 @@ struct GemvArgs {
   float* Y; int64_t ldy; int ypk;         // packed (hidden) or row-major (output layer)
 };
 
+// ---- the layer epilogue of k_fwd for one (row, column) ---------------------------------------
+struct GemvEpi {
+  float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv = 0.f, mxv = 1.f;
+  uint64_t ctr = 0;
+};
+__device__ __forceinline__ void p3d_gemv_epi_load(const GemvArgs& p, int row, int cc, GemvEpi& e) {
+  e.ctr = p.ctr;
+  e.b = p.bias[cc];
+  if (p.bn) { e.gam = p.gamma[cc]; e.bet = p.beta[cc]; e.mmu = p.mmean[cc]; e.mva = p.mvar[cc]; }
+  if (p.res) e.rv = p.res[p3d_pk(row, cc, (p.N + 15) >> 4)];
+  if (p.wsq) e.mxv = *p.wsq;
+  if (p.ctr_dev) e.ctr = (uint64_t)*p.ctr_dev;
+}
+__device__ __forceinline__ float p3d_gemv_epi(const GemvArgs& p, const GemvEpi& e, float zs, int row, int cc) {
+  const float mx = p.wsq ? fmaxf(sqrtf(e.mxv), 1.0f) : 1.0f;
+  const float z = (p.wsq ? zs / mx : zs) + e.b;
+  float y = z;
+  if (p.bn) {
+    const float inv = (1.0f / sqrtf(e.mva + p.eps)) * e.gam;
+    const float shift = e.bet - e.mmu * inv;
+    y = z * inv + shift;
+  }
+  if (p.relu) y = fmaxf(y, 0.0f);
+  if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, p3d_uniform(p.seed, e.ctr, p.site, p.row_off + row, cc));
+  if (p.res) y += e.rv;
+  return y;
+}
+
+// ---- this wave's share of the contraction (k_gemv's chain) -----------------------------------
+// acc[r] += sum over groups g in [gb, ge) (ascending), components x..w, of the lane's fragment
+// times xat(g, r) = x[r][16g + 4q .. +3]; the first GC fragments arrive preloaded in wf.
+template <int MR, int GC, class XAT>
+__device__ __forceinline__ void p3d_gemv_chain(const f32x4* pw, int gb, int ge, int M, f32x4 (&wf)[GC], XAT xat,
+                                               float (&acc)[MR]) {
+  for (int g0 = gb; g0 < ge; g0 += GC) {
+    if (g0 != gb) {
+#pragma unroll
+      for (int j = 0; j < GC; ++j) {
+        const int g = g0 + j < ge ? g0 + j : ge - 1;
+        wf[j] = pw[(int64_t)g * 64];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GC; ++j) {
+      if (g0 + j >= ge) break;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        if (r >= M) break;
+        const f32x4 xv = xat(g0 + j, r);
+        float a = acc[r];
+        a = fmaf(wf[j].x, xv.x, a);
+        a = fmaf(wf[j].y, xv.y, a);
+        a = fmaf(wf[j].z, xv.z, a);
+        a = fmaf(wf[j].w, xv.w, a);
+        acc[r] = a;
+      }
+    }
+  }
+}
+template <int GC>
+__device__ __forceinline__ void p3d_gemv_preload(const f32x4* pw, int gb, int ge, f32x4 (&wf)[GC]) {
+#pragma unroll
+  for (int j = 0; j < GC; ++j) {
+    const int g = gb + j < ge ? gb + j : ge - 1;
+    wf[j] = pw[(int64_t)g * 64];   // default policy: frame after frame hits the XCD's L2 / MALL
+  }
+}
+
 // MR: most rows per launch (B <= MR); WV: waves per workgroup; GC: K groups requested per
 // chunk and wave (registers: 4 * GC).
 template <int MR, int WV, int GC>
@@ -55,45 +135,22 @@ __global__ __launch_bounds__(64 * WV) void k_gemv(GemvArgs p) {
   const int col = 16 * ct + i;
   const bool cok = col < p.N;
   const int cc = cok ? col : p.N - 1;
-  float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv = 0.f, mxv = 1.f;
-  uint64_t ctr = p.ctr;
-  if (w == 0 && q < M) {
-    b = p.bias[cc];
-    if (p.bn) { gam = p.gamma[cc]; bet = p.beta[cc]; mmu = p.mmean[cc]; mva = p.mvar[cc]; }
-    if (p.res) rv = p.res[p3d_pk(q, cc, (p.N + 15) >> 4)];
-    if (p.wsq) mxv = *p.wsq;
-    if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
-  }
+  GemvEpi e;
+  e.ctr = p.ctr;
+  if (w == 0 && q < M) p3d_gemv_epi_load(p, q, cc, e);
   // ---- contraction: this wave's K groups, GC fragments in flight per chunk -----------------
   float acc[MR];
 #pragma unroll
   for (int r = 0; r < MR; ++r) acc[r] = 0.f;
   const f32x4* pw = (const f32x4*)p.Wf + (int64_t)ct * ngK * 64 + lane;
-  for (int g0 = gb; g0 < ge; g0 += GC) {
-    f32x4 wf[GC];
-#pragma unroll
-    for (int j = 0; j < GC; ++j) {
-      const int g = g0 + j < ge ? g0 + j : ge - 1;
-      wf[j] = pw[(int64_t)g * 64];   // default policy: frame after frame hits the XCD's L2 / MALL
-    }
-#pragma unroll
-    for (int j = 0; j < GC; ++j) {
-      if (g0 + j >= ge) break;
-      const int k = 16 * (g0 + j) + 4 * q;
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        if (r >= M) break;
-        const f32x4 xv = p.xpk ? *(const f32x4*)(p.X + ((int64_t)(g0 + j) << 8) + ((r + 16 * q) << 2))
-                               : *(const f32x4*)(p.X + (int64_t)r * p.ldx + k);
-        float a = acc[r];
-        a = fmaf(wf[j].x, xv.x, a);
-        a = fmaf(wf[j].y, xv.y, a);
-        a = fmaf(wf[j].z, xv.z, a);
-        a = fmaf(wf[j].w, xv.w, a);
-        acc[r] = a;
-      }
-    }
-  }
+  f32x4 wf[GC];
+  p3d_gemv_preload<GC>(pw, gb, ge, wf);
+  if (p.xpk)
+    p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
+      return *(const f32x4*)(p.X + ((int64_t)g << 8) + ((r + 16 * q) << 2)); }, acc);
+  else
+    p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
+      return *(const f32x4*)(p.X + (int64_t)r * p.ldx + 16 * g + 4 * q); }, acc);
   // ---- quarters, then waves in fixed order ------------------------------------------------
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
@@ -109,19 +166,370 @@ __global__ __launch_bounds__(64 * WV) void k_gemv(GemvArgs p) {
   float zs = 0.f;
 #pragma unroll
   for (int u = 0; u < WV; ++u) zs += red[u][q][i];
-  // ---- epilogue of k_fwd for row q, column col ---------------------------------------------
-  const float mx = p.wsq ? fmaxf(sqrtf(mxv), 1.0f) : 1.0f;
-  const float z = (p.wsq ? zs / mx : zs) + b;
-  float y = z;
-  if (p.bn) {
-    const float inv = (1.0f / sqrtf(mva + p.eps)) * gam;
-    const float shift = bet - mmu * inv;
-    y = z * inv + shift;
-  }
-  if (p.relu) y = fmaxf(y, 0.0f);
-  if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, p3d_uniform(p.seed, ctr, p.site, p.row_off + q, cc));
-  if (p.res) y += rv;
+  const float y = p3d_gemv_epi(p, e, zs, q, cc);
   if (!cok) return;
   if (p.ypk) p.Y[p3d_pk(q, col, (p.N + 15) >> 4)] = y;
   else p.Y[(int64_t)q * p.ldy + col] = y;
+}
+
+// ---- the folded first / last hidden layers (k_gemv_fold) -------------------------------------
+#define P3D_GEMV_FOLD_MAXK 4096   // largest hidden width the fold's LDS image holds
+#define P3D_GEMV_FOLD_MAXIN 32    // the input width the input-layer fold takes (HUMAN_2D_SIZE)
+
+struct GemvFold {
+  int fin;            // 1: this (first hidden) layer's workgroups compute the input layer themselves
+  GemvArgs in;        //    the input layer: X = the user rows (row-major), Y = act[0] (packed) or null
+  int fout;           // 1: workgroup gridDim.x - 1 runs the output layer on this layer's outputs
+  GemvArgs out;       //    the output layer: Y = the user's y (row-major); X unused
+  float* hand;        // this workspace slot's hand-off: [4 rows][N / 2] 16-B granules {a, tag, b, tag}
+  unsigned* epoch;    // this slot's epoch word (tag = epoch + 1), advanced by the consumer
+  int* err;           // host-visible error word: 1 = the consumer's spin ran out
+};
+
+// The input layer (K = 32) for feature f of row r, as k_gemv<MR, 2, GC> computes it (wave w of
+// two contracts group w in one fmaf chain per quarter q; the quarters sum as (a0 + a1) + (a2 + a3),
+// the two waves as (0 + t0) + t1); x rows staged in xin.
+__device__ __forceinline__ float p3d_gemv_in_value(const GemvArgs& in, const float (*xin)[P3D_GEMV_FOLD_MAXIN],
+                                                   const f32x4 (&wv)[2][4], int r, int f) {
+  GemvEpi e;
+  p3d_gemv_epi_load(in, r, f, e);
+  float zs = 0.f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 xv = *(const f32x4*)&xin[r][16 * g + 4 * q];
+      float s = 0.f;
+      s = fmaf(wv[g][q].x, xv.x, s);
+      s = fmaf(wv[g][q].y, xv.y, s);
+      s = fmaf(wv[g][q].z, xv.z, s);
+      s = fmaf(wv[g][q].w, xv.w, s);
+      a[q] = s;
+    }
+    const float t = (a[0] + a[1]) + (a[2] + a[3]);
+    zs += t;
+  }
+  return p3d_gemv_epi(in, e, zs, r, f);
+}
+__device__ __forceinline__ void p3d_gemv_in_weights(const GemvArgs& in, int f, f32x4 (&wv)[2][4]) {
+  const f32x4* pw = (const f32x4*)in.Wf + (int64_t)(f >> 4) * 2 * 64 + (f & 15);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv[g][q] = pw[g * 64 + 16 * q];
+}
+template <int NT>
+__device__ __forceinline__ void p3d_gemv_stage_x(const GemvArgs& in, float (*xin)[P3D_GEMV_FOLD_MAXIN]) {
+  for (int t = threadIdx.x; t < in.M * P3D_GEMV_FOLD_MAXIN; t += NT)
+    xin[t / P3D_GEMV_FOLD_MAXIN][t % P3D_GEMV_FOLD_MAXIN] =
+        in.X[(int64_t)(t / P3D_GEMV_FOLD_MAXIN) * in.ldx + t % P3D_GEMV_FOLD_MAXIN];
+  __syncthreads();
+}
+
+// The whole input layer, rows r < M, into xs[r][feature]; the columns of column tile `own` also to
+// in.Y (if set).
+template <int MR, int NT>
+__device__ __forceinline__ void p3d_gemv_fold_in(const GemvArgs& in, int own, float* xs, float (*xin)[P3D_GEMV_FOLD_MAXIN]) {
+  const int M = in.M, N = in.N;
+  p3d_gemv_stage_x<NT>(in, xin);
+  for (int f = threadIdx.x; f < N; f += NT) {
+    f32x4 wv[2][4];
+    p3d_gemv_in_weights(in, f, wv);
+#pragma unroll 1
+    for (int r = 0; r < MR; ++r) {   // (rolled: one row's epilogue operands live at a time)
+      if (r >= M) break;
+      const float y = p3d_gemv_in_value(in, xin, wv, r, f);
+      xs[r * N + f] = y;
+      if (in.Y && (f >> 4) == own) in.Y[p3d_pk(r, f, N >> 4)] = y;
+    }
+  }
+  __syncthreads();
+}
+
+// Every thread of the workgroup: rows r < M of a K-wide layer output handed over as granules
+// (granule j of row r = features 2j, 2j + 1, at rh + 16 (gbase + r K / 2 + j)) into xs[r][k], each
+// once its tag matches; then a barrier.
+template <int NT>
+__device__ __forceinline__ void p3d_gemv_gather(__amdgpu_buffer_rsrc_t rh, int gbase, int M, int K, unsigned tag,
+                                                float* xs, int* err) {
+  const int ng = M * (K >> 1);
+  for (int base = 0; base < ng; base += NT) {
+    const int j = base + (int)threadIdx.x;
+    if (j < ng) {
+      u32x4_t v;
+      for (int spin = 0;; ++spin) {
+        v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rh, (gbase + j) * 16, 0, 16));   // sc1
+        if (v.y == tag && v.w == tag) break;
+        if (spin > P3D_XCHG_SPIN) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const int r = j / (K >> 1), k = 2 * (j - r * (K >> 1));
+      xs[r * K + k] = __uint_as_float(v.x);
+      xs[r * K + k + 1] = __uint_as_float(v.z);
+    }
+  }
+  __syncthreads();
+}
+
+// Wave 0 of a tile's workgroup, all 64 lanes: lane (i even, q < M) stores columns col, col + 1 of
+// row q as one sc1 granule {y(col), tag, y(col + 1), tag} at granule gbase + q N / 2 + col / 2.
+__device__ __forceinline__ void p3d_gemv_publish(__amdgpu_buffer_rsrc_t rh, int gbase, int M, int N, int col, float y,
+                                                 unsigned tag) {
+  const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
+  const float y1 = __shfl_down(y, 1, 64);
+  if (q < M && (i & 1) == 0 && col < N) {
+    const u32x4_t v = {__float_as_uint(y), tag, __float_as_uint(y1), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rh, (gbase + q * (N >> 1) + (col >> 1)) * 16, 0, 16);  // sc1
+  }
+}
+
+// The output layer, by one workgroup: its weights first, then the hand-off of the M x K inputs
+// (this launch's other workgroups' outputs) into xs, then every 16-column tile as k_gemv<MR, WV, GC>
+// computes it (the same K split over the WV waves, the same chains and sums).
+template <int MR, int WV, int GC>
+__device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned tag, float* xs,
+                                                  float (*red)[WV][MR][16]) {
+  const GemvArgs& o = f.out;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int M = o.M, K = o.K, ngK = K >> 4, nto = (o.N + 15) >> 4;   // nto <= 4
+  const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
+  GemvEpi e[4];
+  f32x4 wf[4][GC];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= nto) break;
+    const int col = 16 * t + i, cc = col < o.N ? col : o.N - 1;
+    e[t].ctr = o.ctr;
+    if (w == 0 && q < M) p3d_gemv_epi_load(o, q, cc, e[t]);
+    p3d_gemv_preload<GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, wf[t]);
+  }
+  // ---- the hand-off: this launch's other workgroups' outputs ----------------------------------
+  p3d_gemv_gather<64 * WV>(p3d_rsrc(f.hand), 0, M, K, tag, xs, f.err);
+  // every workgroup of the launch has read the epoch (each producer tagged with it): the slot's
+  // next launch gets a new tag
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= nto) break;
+    float acc[MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) acc[r] = 0.f;
+    p3d_gemv_chain<MR, GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, M, wf[t],
+                           [&](int g, int r) { return *(const f32x4*)&xs[r * K + 16 * g + 4 * q]; }, acc);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      acc[r] += __shfl_xor(acc[r], 16, 64);
+      acc[r] += __shfl_xor(acc[r], 32, 64);
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int r = 0; r < MR; ++r) red[t][w][r][i] = acc[r];
+    }
+  }
+  __syncthreads();
+  if (w != 0 || q >= M || q >= MR) return;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= nto) break;
+    const int col = 16 * t + i;
+    float zs = 0.f;
+#pragma unroll
+    for (int u = 0; u < WV; ++u) zs += red[t][u][q][i];
+    const float y = p3d_gemv_epi(o, e[t], zs, q, col < o.N ? col : o.N - 1);
+    if (col < o.N) o.Y[(int64_t)q * o.ldy + col] = y;
+  }
+}
+
+// A hidden layer as k_gemv<MR, WV, GC> (the same bits), with the input layer folded in ahead of it
+// (f.fin) and / or the output layer behind it (f.fout: grid N/16 + 1, the last workgroup runs it).
+template <int MR, int WV, int GC>
+__global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
+  __shared__ float xs[MR * P3D_GEMV_FOLD_MAXK];
+  __shared__ float red[4][WV][MR][16];
+  __shared__ float xin[MR][P3D_GEMV_FOLD_MAXIN];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const unsigned tag = f.fout ? __hip_atomic_load(f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
+  if (f.fout && blockIdx.x == gridDim.x - 1) {
+    p3d_gemv_fold_out<MR, WV, GC>(f, tag, xs, red);
+    return;
+  }
+  const int ct = blockIdx.x;
+  const int ngK = p.K >> 4;
+  const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
+  const int M = p.M;
+  const int col = 16 * ct + i;
+  const bool cok = col < p.N;
+  const int cc = cok ? col : p.N - 1;
+  GemvEpi e;
+  e.ctr = p.ctr;
+  if (!f.fin && w == 0 && q < M) p3d_gemv_epi_load(p, q, cc, e);
+  float acc[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) acc[r] = 0.f;
+  const f32x4* pw = (const f32x4*)p.Wf + (int64_t)ct * ngK * 64 + lane;
+  f32x4 wf[GC];
+  // (with the input layer folded in: requested once that is done -- held in registers across it,
+  // 17 of them spill at 1024 threads)
+  if (!f.fin) p3d_gemv_preload<GC>(pw, gb, ge, wf);
+  if (f.fin) {
+    p3d_gemv_fold_in<MR, 64 * WV>(f.in, ct, xs, xin);
+    p3d_gemv_preload<GC>(pw, gb, ge, wf);
+    if (w == 0 && q < M) p3d_gemv_epi_load(p, q, cc, e);   // (after: fewer registers live across it)
+    const int K = p.K;
+    p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
+      return *(const f32x4*)&xs[r * K + 16 * g + 4 * q]; }, acc);
+  } else {
+    p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
+      return *(const f32x4*)(p.X + ((int64_t)g << 8) + ((r + 16 * q) << 2)); }, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    acc[r] += __shfl_xor(acc[r], 16, 64);
+    acc[r] += __shfl_xor(acc[r], 32, 64);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int r = 0; r < MR; ++r) red[0][w][r][i] = acc[r];
+  }
+  __syncthreads();
+  if (w != 0) return;
+  float zs = 0.f;
+#pragma unroll
+  for (int u = 0; u < WV; ++u) zs += red[0][u][q][i];
+  const float y = p3d_gemv_epi(p, e, zs, q, cc);   // (lanes q >= M: unused)
+  if (!f.fout) {
+    if (q < M && cok) p.Y[p3d_pk(q, col, (p.N + 15) >> 4)] = y;
+    return;
+  }
+  p3d_gemv_publish(p3d_rsrc(f.hand), 0, M, p.N, col, y, tag);   // hand-off to the last workgroup
+}
+
+// ---- the whole batch <= 4 forward as ONE launch (k_gemv_chain) --------------------------------
+// Where every hidden layer's column tiles fit on the device at once (H L / 16 <= CUs: cfg2's four
+// 1024-wide layers are exactly 256 workgroups), workgroup (layer l, tile t) requests its 64 KB
+// weight slice at kernel start -- all H layers' weights stream in together, not one layer's per
+// launch (a k_gemv launch is bound by its 64 CUs' intake of 64 KB each) -- then waits for layer
+// l - 1's outputs as data-tagged granules (layer 1: computes the input layer itself, as k_gemv_fold),
+// contracts, and hands its 16 columns on.  The second layer of a residual block adds the block
+// input's tile: layer 2 recomputes its 16 input-layer columns, later ones read them from the
+// hand-off of layer l - 2.  Workgroup 0 (layer 1, tile 0; idle once its tile is out) then runs the
+// output layer on the last layer's hand-off (p3d_gemv_fold_out) and advances the slot's epoch: every
+// workgroup has read the epoch by then (each published with its tag, and each layer's tiles were
+// all gathered by the next layer's).  Layer l's workgroups wait only for layer l - 1's, which the
+// in-order dispatch placed before them, and every wait is bounded (err).  Same k_gemv arithmetic
+// throughout, so the same bits as the six launches (tests/test_gpu_parity.py::test_gemv_small_batch).
+#define P3D_GEMV_CHAIN_MAXH 8
+#define P3D_GEMV_CHAIN_MAXK 2048   // (L = 2048: the second half of each wave's slice requested after the first's FMAs)
+struct GemvChain {
+  GemvArgs in;                          // layer 0 (X = the user rows, row-major)
+  GemvArgs ly[P3D_GEMV_CHAIN_MAXH];     // hidden layers 1 .. H (X, res, Y unused: handed over)
+  GemvArgs out;                         // the output layer (Y = the user's y, row-major)
+  int H, T;                             // hidden layers; column tiles per layer (L / 16)
+  int res;                              // residual blocks: layer l even adds layer l - 2's output
+  float* hand;                          // this slot: [H][4 rows][L / 2] 16-B granules
+  unsigned* epoch;                      // this slot's epoch word (tag = epoch + 1)
+  int* err;
+};
+
+template <int MR, int GC>
+__global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
+  constexpr int WV = 16;
+  __shared__ float xs[MR * P3D_GEMV_CHAIN_MAXK];
+  __shared__ float red[4][WV][MR][16];
+  __shared__ float xin[MR][P3D_GEMV_FOLD_MAXIN];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const unsigned tag = __hip_atomic_load(c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int b = blockIdx.x, l = 1 + b / c.T, t = b - (l - 1) * c.T;
+  // this layer's arguments, read with constant indices only (a runtime index into the argument
+  // block would copy it to scratch)
+  GemvArgs p = c.ly[0];
+#pragma unroll
+  for (int k = 1; k < P3D_GEMV_CHAIN_MAXH; ++k)
+    if (k == l - 1) p = c.ly[k];
+  const int M = p.M, K = p.K, N = p.N, ngK = K >> 4;
+  const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
+  const int col = 16 * t + i;
+  const __amdgpu_buffer_rsrc_t rh = p3d_rsrc(c.hand);
+  const int gpl = 4 * (N >> 1);                  // granules per layer
+  // ---- the weight slice, then the epilogue operands (wave 0, lane (i, q) = row q, column col) ---
+  // (layer 1: after the input layer -- its weights held across that phase would spill)
+  const f32x4* pw = (const f32x4*)p.Wf + (int64_t)t * ngK * 64 + lane;
+  f32x4 wf[GC];
+  if (l != 1) p3d_gemv_preload<GC>(pw, gb, ge, wf);
+  GemvEpi e;
+  e.ctr = p.ctr;
+  if (l != 1 && w == 0 && q < M) p3d_gemv_epi_load(p, q, col, e);
+  // ---- the residual tile (wave 0): layer 2 recomputes the input layer's, later layers read theirs
+  const bool second = c.res && l >= 2 && (l & 1) == 0;
+  float rv = 0.f;
+  if (second && l > 2 && w == 0 && q < M) {
+    const u32x4_t v0 = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+        rh, ((l - 3) * gpl + q * (N >> 1) + (col >> 1)) * 16, 0, 16));
+    u32x4_t v = v0;
+    for (int spin = 0; !(v.y == tag && v.w == tag); ++spin) {
+      if (spin > P3D_XCHG_SPIN) { __hip_atomic_store(c.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
+      __builtin_amdgcn_s_sleep(1);
+      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+          rh, ((l - 3) * gpl + q * (N >> 1) + (col >> 1)) * 16, 0, 16));
+    }
+    rv = __uint_as_float((i & 1) ? v.z : v.x);
+  }
+  // ---- this layer's input --------------------------------------------------------------------
+  if (l == 1) {
+    GemvArgs in = c.in;
+    in.Y = nullptr;
+    p3d_gemv_fold_in<MR, 64 * WV>(in, -1, xs, xin);
+    p3d_gemv_preload<GC>(pw, gb, ge, wf);
+    if (w == 0 && q < M) p3d_gemv_epi_load(p, q, col, e);
+  } else {
+    if (second && l == 2) {
+      p3d_gemv_stage_x<64 * WV>(c.in, xin);
+      if (w == 0 && q < M) {
+        f32x4 wv[2][4];
+        p3d_gemv_in_weights(c.in, col, wv);
+        rv = p3d_gemv_in_value(c.in, xin, wv, q, col);
+      }
+    }
+    p3d_gemv_gather<64 * WV>(rh, (l - 2) * gpl, M, K, tag, xs, c.err);
+  }
+  // ---- contraction, quarters, waves (k_gemv) -------------------------------------------------
+  float acc[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) acc[r] = 0.f;
+  p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
+    return *(const f32x4*)&xs[r * K + 16 * g + 4 * q]; }, acc);
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    acc[r] += __shfl_xor(acc[r], 16, 64);
+    acc[r] += __shfl_xor(acc[r], 32, 64);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int r = 0; r < MR; ++r) red[0][w][r][i] = acc[r];
+  }
+  __syncthreads();
+  if (w == 0) {
+    float zs = 0.f;
+#pragma unroll
+    for (int u = 0; u < WV; ++u) zs += red[0][u][q][i];
+    float y = p3d_gemv_epi(p, e, zs, q, col);   // (p.res is null: the residual is added last, as there)
+    if (second) y += rv;
+    p3d_gemv_publish(rh, (l - 1) * gpl, M, N, col, y, tag);
+  }
+  if (b != 0) return;
+  // ---- workgroup 0: the output layer on the last layer's hand-off -------------------------------
+  GemvFold f{};
+  f.fout = 1;
+  f.out = c.out;
+  f.hand = c.hand + (int64_t)(c.H - 1) * gpl * 4;
+  f.epoch = c.epoch;
+  f.err = c.err;
+  p3d_gemv_fold_out<MR, WV, 4>(f, tag, xs, red);
 }

@@ -91,6 +91,16 @@ def test_eval_forward_large_batch(B, residual, batch_norm, max_norm, keep):
     m.close()
 
 
+def _gemv_tags(m, fn):
+    import ctypes
+    import _p3d
+    _p3d.check(_p3d.lib().p3d_profile_start(m._h, 64), "p3d_profile_start")
+    out = fn()
+    buf = ctypes.create_string_buffer(1 << 12)
+    _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
+    return out, {ln.split("\t")[0]: int(ln.split("\t")[1]) for ln in buf.value.decode().strip().splitlines()}
+
+
 @pytest.mark.parametrize("L,N,B,residual,batch_norm,max_norm,keep,p14", [
     (1024, 2, 1, True, True, False, 1.0, False), (1024, 2, 2, True, True, False, 1.0, False),
     (1024, 2, 3, True, True, True, 1.0, False), (1024, 2, 4, True, True, False, 0.5, False),
@@ -99,22 +109,25 @@ def test_eval_forward_large_batch(B, residual, batch_norm, max_norm, keep):
 def test_gemv_small_batch(L, N, B, residual, batch_norm, max_norm, keep, p14, monkeypatch):
     """Batch <= 4 inference through the weight-streaming k_gemv layers (the per-frame call of
     src/openpose_3dpose_sandbox.py:353-356) vs the fp64 oracle; rows independent (every row
-    bit-identical to its own batch-1 call, also from another workspace row); agreement with
-    the 16-row MFMA kernels (P3D_GEMV_MAXB=0) within the same tolerance."""
+    bit-identical to its own batch-1 call, also from another workspace row); the one-launch
+    persistent chain (k_gemv_chain, where the hidden layers' tiles fit on the device), the
+    four-launch fold (input / output layers inside the first / last hidden layer's k_gemv_fold)
+    and the six plain launches give the same bits; agreement with the 16-row
+    MFMA kernels (P3D_GEMV_MAXB=0) within the same tolerance."""
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
                       predict_14=p14)
     st, m = make(cfg, batch=B, max_batch=64)
     rng = np.random.default_rng(100 + B)
     x = rng.standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
-    import ctypes
-    import _p3d
-    _p3d.check(_p3d.lib().p3d_profile_start(m._h, 64), "p3d_profile_start")
-    y = m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy()
-    buf = ctypes.create_string_buffer(1 << 12)
-    _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
-    tags = {ln.split("\t")[0]: int(ln.split("\t")[1]) for ln in buf.value.decode().strip().splitlines()}
-    assert tags == {"gemv_in": 1, "gemv_hidden": 2 * N, "gemv_out": 1}, tags
+    y, tags = _gemv_tags(m, lambda: m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy())
+    fold = {"gemv_in_hidden": 1, "gemv_hidden_out": 1}
+    if N > 1:
+        fold["gemv_hidden"] = 2 * N - 2
+    chain = (os.environ.get("P3D_GEMV_CHAIN", "0") == "1"
+             and 2 * N * (L // 16) <= torch.cuda.get_device_properties(0).multi_processor_count)
+    assert tags == ({"gemv_chain": 1} if chain else fold), tags
+    m.check_errors()
     ro, _ = ref_mlp.forward(st, x, False, keep, m.seed, 3, 8)
     close(y, ro)
     for r in range(B):
@@ -123,7 +136,27 @@ def test_gemv_small_batch(L, N, B, residual, batch_norm, max_norm, keep, p14, mo
     y16 = torch.empty((B, m.output_size), dtype=torch.float32, device="cuda")
     m.forward_device(xd, False, keep, ctr=3, row_offset=8, out=y16, ws_row=16)
     np.testing.assert_array_equal(y16.cpu().numpy(), y)
+    for _ in range(3):   # the same slot again and again (epoch-tagged hand-off): the same bits
+        np.testing.assert_array_equal(m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy(), y)
+    m.check_errors()
     m.close()
+    # the same bits from: the four-launch fold, the six plain launches
+    for env, want in (({"P3D_GEMV_CHAIN": "0"}, fold),
+                      ({"P3D_GEMV_FOLD": "0"}, {"gemv_in": 1, "gemv_hidden": 2 * N, "gemv_out": 1})):
+        saved = {k: os.environ.get(k) for k in ("P3D_GEMV_CHAIN", "P3D_GEMV_FOLD")}
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        st, m = make(cfg, batch=B, max_batch=64)
+        yf, tags = _gemv_tags(m, lambda: m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy())
+        assert tags == want, (env, tags)
+        np.testing.assert_array_equal(yf, y)
+        m.check_errors()
+        m.close()
+        for k, v in saved.items():
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, v)
     monkeypatch.setenv("P3D_GEMV_MAXB", "0")
     st, m = make(cfg, batch=B, max_batch=64)
     ym = m.forward_device(xd, False, keep, ctr=3, row_offset=8).cpu().numpy()
@@ -228,37 +261,26 @@ def test_train_steps_track_oracle(split, xchg, monkeypatch):
 @pytest.mark.parametrize("L,B,keep,delay", [(1024, 64, 0.5, 0), (256, 17, 0.5, 0), (256, 64, 1.0, 0),
                                            (256, 200, 0.5, 0), (1024, 64, 0.5, 8), (256, 200, 0.5, 8)])
 def test_bn_exchange_bit_identical_to_split(L, B, keep, delay, monkeypatch):
-    """BN-train layers as ONE launch == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit,
-    over 4 fused train steps: outputs, loss, weights, Adam slots, moving statistics.  Two one-launch
-    forms: the K-split form (p3d_ks.h, round 4: 8 sibling workgroups of a column pair each contract
-    one eighth of K for all rows and swap partial products; B <= 64) and the row-tile exchange form
-    (p3d_xchg.h: row-tile workgroups swap column moments; B = 200 there too).  All three run the
-    8-wave association of the hidden data gradient (P3D_DGRAD_WK=8, the K-split form's).  B = 200
-    (13 row tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4.
+    """BN-train layers as ONE launch (row-tile workgroups swap their column statistics in the
+    launch, p3d_xchg.h) == the split form (GEMM + k_bn_fwd / k_bn_bwd), bit for bit, over 4
+    fused train steps: outputs, loss, weights, Adam slots, moving statistics.  B = 200 (13 row
+    tiles x 16 column tiles = 208 workgroups) exercises a ragged last row tile and R > 4.
     delay > 0 (test hook P3D_XCHG_TEST_DELAY): the last row-tile workgroup of every odd column
-    tile of the exchange form sleeps ~27 us before it reads its tag, so other column tiles finish
-    their swaps (and advance their epochs) first -- with one epoch word per site that late
-    sibling read a tag its siblings did not hold (advisor r2); with the column tile's own word it
-    must not matter."""
+    tile sleeps ~27 us before it reads its tag, so other column tiles finish their swaps (and
+    advance their epochs) first -- with one epoch word per site that late sibling read a tag
+    its siblings did not hold (advisor r2); with the column tile's own word it must not matter."""
     import ctypes
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=2, residual=True, batch_norm=True)
     st = ref_mlp.init_state(cfg, seed=6, bn_seed=7)
-    forms = (("ks", {"P3D_TRAIN_XCHG": "1", "P3D_TRAIN_KS": "1"}),
-             ("x", {"P3D_TRAIN_XCHG": "1", "P3D_TRAIN_KS": "0", "P3D_DGRAD_WK": "8", "P3D_XCHG_TEST_DELAY": str(delay)}),
-             ("split", {"P3D_TRAIN_XCHG": "0", "P3D_TRAIN_KS": "1"}))
     ms = []
-    for _, env in forms:
-        for k in ("P3D_TRAIN_XCHG", "P3D_TRAIN_KS", "P3D_DGRAD_WK", "P3D_XCHG_TEST_DELAY"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for flag in ("1", "0"):
+        monkeypatch.setenv("P3D_TRAIN_XCHG", flag)
+        monkeypatch.setenv("P3D_XCHG_TEST_DELAY", str(delay if flag == "1" else 0))
         m = linear_model.LinearModel(L, 2, True, True, False, B, 1e-3, "/tmp/p3d_test", seed=9, max_batch=max(B, 64))
         m.set_weights({**st.params, **st.moving})
         ms.append(m)
-    for k in ("P3D_TRAIN_XCHG", "P3D_TRAIN_KS", "P3D_DGRAD_WK", "P3D_XCHG_TEST_DELAY"):
-        monkeypatch.delenv(k, raising=False)
-    km, xm, sm = ms
+    xm, sm = ms
     rng = np.random.default_rng(L + B)
     for step in range(4):
         x = torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)).cuda()
@@ -272,24 +294,19 @@ def test_bn_exchange_bit_identical_to_split(L, B, keep, delay, monkeypatch):
                 buf = ctypes.create_string_buffer(1 << 14)
                 _p3d.check(_p3d.lib().p3d_profile_stop(m._h, buf, len(buf)), "p3d_profile_stop")
                 m.tags = {ln.split("\t")[0] for ln in buf.value.decode().strip().splitlines()}
-        for (tag, _), y in zip(forms[1:], ys[1:]):
-            assert torch.equal(ys[0], y), (step, tag)
-        assert torch.equal(km._loss_dev, xm._loss_dev) and torch.equal(km._loss_dev, sm._loss_dev), step
-    for m in (km, xm):
-        m.sync_check()
-        m.check_errors()
+        assert torch.equal(ys[0], ys[1]), step
+        assert torch.equal(xm._loss_dev, sm._loss_dev), step
+    xm.sync_check()
+    xm.check_errors()
     for k in ("params", "moving", "adam_m", "adam_v"):
-        if km.flat[k] is not None:
-            assert torch.equal(km.flat[k], xm.flat[k]), k
-            assert torch.equal(km.flat[k], sm.flat[k]), k
-    assert km.get_step() == xm.get_step() == sm.get_step()
-    # the one-launch forms really ran: no second BN launch in either direction
-    want_ks = B <= 64 and L % 256 == 0
-    assert ("fwd_hidden_train_ks" in km.tags) == want_ks, km.tags
-    assert "fwd_hidden_train_x" in xm.tags and not {"bn_fwd", "bn_bwd"} & (xm.tags | km.tags), (xm.tags, km.tags)
+        if xm.flat[k] is not None:
+            assert torch.equal(xm.flat[k], sm.flat[k]), k
+    assert xm.get_step() == sm.get_step()
+    # the exchange form really ran: no second BN launch in either direction
+    assert "fwd_hidden_train_x" in xm.tags and not {"bn_fwd", "bn_bwd"} & xm.tags, xm.tags
     assert {"bn_fwd", "bn_bwd"} <= sm.tags, sm.tags
-    for m in ms:
-        m.close()
+    xm.close()
+    sm.close()
 
 
 @pytest.mark.parametrize("B", [128, 200])
