@@ -624,8 +624,11 @@ class LinearModel(object):
 
     def dp_buckets(self, bucket_mb=None, gloo=False):
         """Enable (bucket_mb > 0) or disable (0) the bucketed gradient all-reduce that
-        overlaps the backward (env P3D_DP_BUCKET_MB, default 8 MB: at cfg2 two buckets, {output,
-        hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two weight-gradient launches;
+        overlaps the backward (env P3D_DP_BUCKET_MB; default 8 MB on a group of several ranks: at
+        cfg2 two buckets, {output, hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two
+        weight-gradient launches; default 0 on a 1-rank group, whose all-reduce is the identity, so
+        buckets would buy no overlap and cost two launches and a second optimizer pass: 122.9 vs
+        115.3 us per cfg3 step, profiles/r04_dp1_bucket_ab.json);
         RCCL by default, gloo -- host-staged, for tests of several ranks on one GPU -- when
         gloo=True).  Under RCCL the model is attached to the library's own communicator
         (dist_utils.native_comm, p3d_dp_attach) and every DP step is one p3d_train_step_dp.
@@ -634,7 +637,11 @@ class LinearModel(object):
         import ctypes
         import torch.distributed as dist
         if bucket_mb is None:
-            bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "8"))
+            env = os.environ.get("P3D_DP_BUCKET_MB")
+            if env is not None:
+                bucket_mb = float(env)
+            else:
+                bucket_mb = 8.0 if dist.is_initialized() and dist.get_world_size() > 1 else 0.0
         nccl = self.data_parallel and dist.is_initialized() and dist.get_backend() == "nccl"
         if nccl and getattr(self, "_native", None) is None:
             self._native = dist_utils.native_comm()

@@ -1057,12 +1057,23 @@ def cpu_data_baseline(seconds):
             "sample": "%d camera-poses (4 sequences x 2600 frames x 4 cameras per pass), %.1f s" % (done, dt)}
 
 
+def model_bucket_mb(args, world):
+    """The gradient-bucket size a DP run uses: --dp-bucket-mb if given, else the library's policy
+    (LinearModel.dp_buckets: 8 MB on several ranks, none on one)."""
+    if args.dp_bucket_mb is not None:
+        return args.dp_bucket_mb
+    env = os.environ.get("P3D_DP_BUCKET_MB")
+    return float(env) if env is not None else (8.0 if world > 1 else 0.0)
+
+
 def run_dp1_child(args, timeout=300):
     """Run the 1-rank data-parallel train leg as `bench.py --dp1-child` (a fresh process; the
     caller has not initialised the GPU) and return its JSON, or {"error": ...}."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--dp1-child", "--train-steps", str(args.train_steps),
-           "--dp-bucket-mb", str(args.dp_bucket_mb), "--keep", str(args.keep)]
+           "--keep", str(args.keep)]
+    if args.dp_bucket_mb is not None:
+        cmd += ["--dp-bucket-mb", str(args.dp_bucket_mb)]
     if args.train_eager:
         cmd.append("--train-eager")
     env = dict(os.environ)
@@ -1089,10 +1100,15 @@ def dp1_child(args, json_fd):
     torch.cuda.set_device(0)
     init_world1_group()
     dv, ddt, droof, dmode = bench_train(args, 0, 1, steps=args.train_steps, warmup=64, dp=True)
-    out = {"workload": "the data-parallel step (fwd + bwd with %g MB gradient buckets, one weight-gradient launch "
-                       "each, RCCL all-reduce from libp3d's own communicator on its comm stream, each bucket's TF1 "
-                       "Adam + re-pack behind its all-reduce on the compute stream, step advance in the last; "
-                       "1-rank group: the reduction is the identity)" % args.dp_bucket_mb,
+    bk = model_bucket_mb(args, 1)
+    form = ("%g MB gradient buckets, one weight-gradient launch each, RCCL all-reduce from libp3d's own "
+            "communicator on its comm stream, each bucket's TF1 Adam + re-pack behind its all-reduce on the "
+            "compute stream" % bk) if bk > 0 else (
+            "one gradient-only weight-gradient launch, the RCCL all-reduce of the flat gradient from libp3d's own "
+            "communicator, TF1 Adam + re-pack behind it (the library's bucket policy on a 1-rank group: no "
+            "buckets, nothing to overlap)")
+    out = {"workload": "the data-parallel step (fwd + bwd, %s; step advance in the last launch; 1-rank group: the "
+                       "reduction is the identity)" % form,
            "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
            "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
            "event_pair_avg_us": droof.get("event_pair_avg_us")}
@@ -1121,8 +1137,9 @@ def build_arg_parser():
     ap.add_argument("--no-dp1", action="store_true", help="skip the 1-rank data-parallel train form (infer mode)")
     ap.add_argument("--train-steps", type=int, default=400, help="train sub-measurement (infer mode)")
     ap.add_argument("--keep", type=float, default=0.5, help="dropout keep_prob of the train step")
-    ap.add_argument("--dp-bucket-mb", type=float, default=8.0,
-                    help="data-parallel gradient all-reduce bucket (MB) overlapping the backward; 0 = one all-reduce")
+    ap.add_argument("--dp-bucket-mb", type=float, default=None,
+                    help="data-parallel gradient all-reduce bucket (MB) overlapping the backward; 0 = one all-reduce "
+                         "(default: the library's policy, 8 MB on several ranks, none on a 1-rank group)")
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
@@ -1197,10 +1214,10 @@ def main():
                 train = {"error": repr(exc)[:300]}
             if dp1 is not None:
                 train["dp_form_1rank"] = dp1
-            if world > 1 and args.dp_bucket_mb > 0 and "error" not in train:
+            if world > 1 and model_bucket_mb(args, world) > 0 and "error" not in train:
                 try:   # the same steps with one all-reduce after the backward (no overlap)
                     sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=0)
-                    train["dp_bucket_mb"] = args.dp_bucket_mb
+                    train["dp_bucket_mb"] = model_bucket_mb(args, world)
                     train["single_allreduce"] = {"value": round(sv, 1), "unit": "poses/s",
                                                  "ms_per_step": round(1000.0 * sdt / args.train_steps, 5)}
                 except Exception as exc:
