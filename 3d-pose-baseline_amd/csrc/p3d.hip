@@ -1692,8 +1692,8 @@ struct p3d_model {
   int gemv_maxb = 4;        // inference at B <= gemv_maxb runs the k_gemv layers (env P3D_GEMV_MAXB, 0..4)
   int gemv_fold = 1;        // ... with the input / output layers folded into the first / last hidden layer's
                             // launch (k_gemv_fold; env P3D_GEMV_FOLD; the same bits either way)
-  int gemv_chain = 0;       // ... as ONE persistent launch where the hidden layers' tiles fit on the device
-                            // (k_gemv_chain; env P3D_GEMV_CHAIN=1, opt-in until validated on the box; the same bits)
+  int gemv_chain = 1;       // ... as ONE persistent launch where the hidden layers' tiles fit on the device
+                            // (k_gemv_chain; env P3D_GEMV_CHAIN; the same bits; cfg2 batch 1: 16.3 vs 21.4 us)
   int gemv_slots = 0;       // workspace slots (ws_row / 16) the fold's hand-off buffer covers (others unfolded)
   int64_t gemv_slot_floats = 0;     // hand-off floats per slot (the chain's H layers, or the fold's one)
   float* gemv_hand = nullptr;       // [slot][layers][4 rows][L / 2] 16-B granules (layer-output hand-offs)

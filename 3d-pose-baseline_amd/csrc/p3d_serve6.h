@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
   const int q4 = 4 * (lane >> 4);
-  const int S = p.split;
+  const int S = min(max(p.split, 1), 8);   // (an out-of-range split is reported below, never divided by)
 #ifdef P3D_TRACE
   const unsigned long long t_start = wall_clock64();
   unsigned long long* tr6 = nullptr;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // test hook (P3D_SERVE_TEST_DELAY): every workgroup of one XCD arrives ~delay x 3.4 us late
     if (p.delay > 0 && xcc == p.delay_xcc)
       for (int i = 0; i < p.delay; ++i) __builtin_amdgcn_s_sleep(127);
-    const bool bad = (gridDim.x & 7u) != 0u || S < 1 || S > 8 || p.census_extra;
+    const bool bad = (gridDim.x & 7u) != 0u || p.split < 1 || p.split > 8 || p.census_extra;
     sh[0] = (int)(((unsigned)xcc - blockIdx.x) & 7u);   // (trace: the launch's starting XCD)
     sh[2] = bad ? 1 : 0;
     sh[4] = 0;                               // some wave of this workgroup is broken (group_sync)
@@ -205,9 +205,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     wq = tid < nl_ec ? p.ecg[(int64_t)nl_ec * T * 48 + tid] : 1.f;
   };
-  int r = 0, n = 1, gid = 0, gi = -1, ng = 0;
-  const bool placeable = (gridDim.x & 7u) == 0u && S >= 1 && S <= 8;
-  if (placeable) place([&](int) { return nxg; }, xcc, rx, r, n, gid, gi, ng);
+  // (unconditional: placement under a guard made the compiler keep its results in a form that cost
+  // the main loop 52 AGPRs of its allocation and ~20 us per launch; gid is only used to address
+  // memory where the launch is placeable)
+  int r, n, gid, gi, ng;
+  const bool placeable = (gridDim.x & 7u) == 0u && p.split >= 1 && p.split <= 8;
+  place([&](int) { return nxg; }, xcc, rx, r, n, gid, gi, ng);
   // The group's epoch word (one per group slot; bank = epoch & 1).  Every member reads it at its
   // start; the group's rank-0 member advances it at the END of its work, by which time every
   // member has read it: rank 0's four waves read the whole K of every hidden layer, i.e. waited
@@ -220,7 +223,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (tid == 0 && placeable) ep = __hip_atomic_load(p.epoch + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the first unit's input-layer operands and the epilogue constants in flight with the epoch read
   prefetch(gi, (T * r) / n, (T * (r + 1)) / n);
-  if (tid == 0) sh[3] = (int)(ep & 1u);
+  if (tid == 0) {
+    sh[3] = (int)(ep & 1u);
+    // the epoch word this workgroup advances at its end (-1: none), parked in LDS: kept in
+    // registers across the whole launch it cost the main loop its register allocation (222 vs
+    // 166 AGPRs, 134 vs 113 us per launch)
+    sh[5] = (placeable && r == 0 && gi >= 0 && gi < p.nb) ? gid : -1;
+  }
   __syncthreads();
 #ifdef P3D_TRACE
   if (tid == 0 && blockIdx.x < 1024) {     // per workgroup: start, placement known, XCD | rank
@@ -653,7 +662,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
   }
-  if (r == 0 && tid == 0 && gi < p.nb)   // (every member has read the epoch by now: see its read)
-    __hip_atomic_fetch_add(p.epoch + gid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && sh[5] >= 0)   // (every member has read the epoch by now: see its read)
+    __hip_atomic_fetch_add(p.epoch + sh[5], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

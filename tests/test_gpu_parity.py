@@ -124,7 +124,7 @@ def test_gemv_small_batch(L, N, B, residual, batch_norm, max_norm, keep, p14, mo
     fold = {"gemv_in_hidden": 1, "gemv_hidden_out": 1}
     if N > 1:
         fold["gemv_hidden"] = 2 * N - 2
-    chain = (os.environ.get("P3D_GEMV_CHAIN", "0") == "1"
+    chain = (os.environ.get("P3D_GEMV_CHAIN", "1") == "1"
              and 2 * N * (L // 16) <= torch.cuda.get_device_properties(0).multi_processor_count)
     assert tags == ({"gemv_chain": 1} if chain else fold), tags
     m.check_errors()
