@@ -437,6 +437,9 @@ struct GemvChain {
   int* err;
 };
 
+// (Measured and rejected: each wave DMAing its fragments into LDS at kernel start -- layer 1 too,
+// ahead of its input layer, with no registers held -- and reading them back for the contraction:
+// 17.5 vs 16.3-16.7 us per forward, A/B on one box, profiles/r04_gemv_chain_ab.json.)
 template <int MR, int GC>
 __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   constexpr int WV = 16;
