@@ -2075,7 +2075,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
       m->gemv_slots = (int)std::min<int64_t>(64, (c.max_batch + 15) / 16);
       const int H = nl - 2;
       const bool chain = H >= 1 && H <= P3D_GEMV_CHAIN_MAXH && L <= P3D_GEMV_CHAIN_MAXK && H * (L / 16) <= m->num_cus;
-      m->gemv_slot_floats = (int64_t)(chain ? H : 1) * 4 * (L / 2) * 4;
+      m->gemv_slot_floats = (int64_t)(chain ? H + 1 : 1) * 4 * (L / 2) * 4;
       const int64_t nh = (int64_t)m->gemv_slots * m->gemv_slot_floats;
       if ((e = hipMalloc(&m->gemv_hand, nh * sizeof(float))) != hipSuccess) return cleanup(e);
       if ((e = hipMemset(m->gemv_hand, 0, nh * sizeof(float))) != hipSuccess) return cleanup(e);
@@ -2607,7 +2607,7 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
                     c.output_size <= 64;
   const int H = nl - 2, T = L / 16;
   if (fold && m->gemv_chain && H <= P3D_GEMV_CHAIN_MAXH && L <= P3D_GEMV_CHAIN_MAXK && H * T <= m->num_cus &&
-      m->gemv_slot_floats >= (int64_t)H * 4 * (L / 2) * 4) {
+      m->gemv_slot_floats >= (int64_t)(H + 1) * 4 * (L / 2) * 4) {
     GemvChain ch{};
     fill(0, x, ch.in);
     ch.in.Y = nullptr;

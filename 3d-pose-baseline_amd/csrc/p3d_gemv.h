@@ -111,6 +111,18 @@ __device__ __forceinline__ void p3d_gemv_chain(const f32x4* pw, int gb, int ge, 
     }
   }
 }
+// Pin values in registers here: the loads that produce them complete at this point and are not
+// re-issued later.  (Without it the compiler sank a persistent kernel's weight and epilogue-operand
+// loads past its hand-off waits, to the point of use: ~0.6 us of load latency per layer on the
+// critical path, 2.7 us for the output layer -- tools/trace_chain.py.)
+template <int GC>
+__device__ __forceinline__ void p3d_pin(f32x4 (&v)[GC]) {
+#pragma unroll
+  for (int j = 0; j < GC; ++j) asm volatile("" : "+v"(v[j]));
+}
+__device__ __forceinline__ void p3d_pin_epi(GemvEpi& e) {
+  asm volatile("" : "+v"(e.b), "+v"(e.gam), "+v"(e.bet), "+v"(e.mmu), "+v"(e.mva), "+v"(e.rv), "+v"(e.mxv));
+}
 template <int GC>
 __device__ __forceinline__ void p3d_gemv_preload(const f32x4* pw, int gb, int ge, f32x4 (&wf)[GC]) {
 #pragma unroll
@@ -189,10 +201,9 @@ struct GemvFold {
 // The input layer (K = 32) for feature f of row r, as k_gemv<MR, 2, GC> computes it (wave w of
 // two contracts group w in one fmaf chain per quarter q; the quarters sum as (a0 + a1) + (a2 + a3),
 // the two waves as (0 + t0) + t1); x rows staged in xin.
+// (e: the feature's epilogue operands, row-independent -- the input layer has no residual)
 __device__ __forceinline__ float p3d_gemv_in_value(const GemvArgs& in, const float (*xin)[P3D_GEMV_FOLD_MAXIN],
-                                                   const f32x4 (&wv)[2][4], int r, int f) {
-  GemvEpi e;
-  p3d_gemv_epi_load(in, r, f, e);
+                                                   const f32x4 (&wv)[2][4], const GemvEpi& e, int r, int f) {
   float zs = 0.f;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -200,6 +211,29 @@ __device__ __forceinline__ float p3d_gemv_in_value(const GemvArgs& in, const flo
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4 xv = *(const f32x4*)&xin[r][16 * g + 4 * q];
+      float s = 0.f;
+      s = fmaf(wv[g][q].x, xv.x, s);
+      s = fmaf(wv[g][q].y, xv.y, s);
+      s = fmaf(wv[g][q].z, xv.z, s);
+      s = fmaf(wv[g][q].w, xv.w, s);
+      a[q] = s;
+    }
+    const float t = (a[0] + a[1]) + (a[2] + a[3]);
+    zs += t;
+  }
+  return p3d_gemv_epi(in, e, zs, r, f);
+}
+// the same with x read from in.X (for one feature per lane: no staging)
+__device__ __forceinline__ float p3d_gemv_in_value_g(const GemvArgs& in, const f32x4 (&wv)[2][4], const GemvEpi& e,
+                                                     int r, int f) {
+  const float* xr = in.X + (int64_t)r * in.ldx;
+  float zs = 0.f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 xv = *(const f32x4*)(xr + 16 * g + 4 * q);
       float s = 0.f;
       s = fmaf(wv[g][q].x, xv.x, s);
       s = fmaf(wv[g][q].y, xv.y, s);
@@ -228,22 +262,35 @@ __device__ __forceinline__ void p3d_gemv_stage_x(const GemvArgs& in, float (*xin
 }
 
 // The whole input layer, rows r < M, into xs[r][feature]; the columns of column tile `own` also to
-// in.Y (if set).
-template <int MR, int NT>
-__device__ __forceinline__ void p3d_gemv_fold_in(const GemvArgs& in, int own, float* xs, float (*xin)[P3D_GEMV_FOLD_MAXIN]) {
+// in.Y (if set).  The thread's first feature's weights and epilogue operands are requested before
+// the x rows are staged (one memory round trip, not two); post() runs once the features are done,
+// before the closing barrier (the caller's next requests in flight across it).
+template <int MR, int NT, class POST>
+__device__ __forceinline__ void p3d_gemv_fold_in(const GemvArgs& in, int own, float* xs, float (*xin)[P3D_GEMV_FOLD_MAXIN],
+                                                 POST post) {
   const int M = in.M, N = in.N;
+  const int f0 = threadIdx.x;
+  f32x4 wv[2][4];
+  GemvEpi e;
+  if (f0 < N) {
+    p3d_gemv_in_weights(in, f0, wv);
+    p3d_gemv_epi_load(in, 0, f0, e);
+  }
   p3d_gemv_stage_x<NT>(in, xin);
-  for (int f = threadIdx.x; f < N; f += NT) {
-    f32x4 wv[2][4];
-    p3d_gemv_in_weights(in, f, wv);
+  for (int f = f0; f < N; f += NT) {
+    if (f != f0) {
+      p3d_gemv_in_weights(in, f, wv);
+      p3d_gemv_epi_load(in, 0, f, e);
+    }
 #pragma unroll 1
-    for (int r = 0; r < MR; ++r) {   // (rolled: one row's epilogue operands live at a time)
+    for (int r = 0; r < MR; ++r) {
       if (r >= M) break;
-      const float y = p3d_gemv_in_value(in, xin, wv, r, f);
+      const float y = p3d_gemv_in_value(in, xin, wv, e, r, f);
       xs[r * N + f] = y;
       if (in.Y && (f >> 4) == own) in.Y[p3d_pk(r, f, N >> 4)] = y;
     }
   }
+  post();
   __syncthreads();
 }
 
@@ -308,8 +355,17 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     if (w == 0 && q < M) p3d_gemv_epi_load(o, q, cc, e[t]);
     p3d_gemv_preload<GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, wf[t]);
   }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= nto) break;
+    p3d_pin<GC>(wf[t]);
+    p3d_pin_epi(e[t]);
+  }
   // ---- the hand-off: this launch's other workgroups' outputs ----------------------------------
   p3d_gemv_gather<64 * WV>(p3d_rsrc(f.hand), 0, M, K, tag, xs, f.err);
+#ifdef P3D_TRACE
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_p3d_trace[4] = wall_clock64();
+#endif
   // every workgroup of the launch has read the epoch (each producer tagged with it): the slot's
   // next launch gets a new tag
   if (threadIdx.x == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -378,8 +434,7 @@ __global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
   // 17 of them spill at 1024 threads)
   if (!f.fin) p3d_gemv_preload<GC>(pw, gb, ge, wf);
   if (f.fin) {
-    p3d_gemv_fold_in<MR, 64 * WV>(f.in, ct, xs, xin);
-    p3d_gemv_preload<GC>(pw, gb, ge, wf);
+    p3d_gemv_fold_in<MR, 64 * WV>(f.in, ct, xs, xin, [&] { p3d_gemv_preload<GC>(pw, gb, ge, wf); });
     if (w == 0 && q < M) p3d_gemv_epi_load(p, q, cc, e);   // (after: fewer registers live across it)
     const int K = p.K;
     p3d_gemv_chain<MR, GC>(pw, gb, ge, M, wf, [&](int g, int r) {
@@ -415,15 +470,17 @@ __global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
 // 1024-wide layers are exactly 256 workgroups), workgroup (layer l, tile t) requests its 64 KB
 // weight slice at kernel start -- all H layers' weights stream in together, not one layer's per
 // launch (a k_gemv launch is bound by its 64 CUs' intake of 64 KB each) -- then waits for layer
-// l - 1's outputs as data-tagged granules (layer 1: computes the input layer itself, as k_gemv_fold),
-// contracts, and hands its 16 columns on.  The second layer of a residual block adds the block
-// input's tile: layer 2 recomputes its 16 input-layer columns, later ones read them from the
-// hand-off of layer l - 2.  Workgroup 0 (layer 1, tile 0; idle once its tile is out) then runs the
-// output layer on the last layer's hand-off (p3d_gemv_fold_out) and advances the slot's epoch: every
-// workgroup has read the epoch by then (each published with its tag, and each layer's tiles were
-// all gathered by the next layer's).  Layer l's workgroups wait only for layer l - 1's, which the
-// in-order dispatch placed before them, and every wait is bounded (err).  Same k_gemv arithmetic
-// throughout, so the same bits as the six launches (tests/test_gpu_parity.py::test_gemv_small_batch).
+// l - 1's outputs as data-tagged granules, contracts, and hands its 16 columns on.  The input layer
+// (K = 32) is computed by layer 2's workgroups, tile t each, as their first act (hand-off slot 0):
+// recomputing all of it in every layer-1 workgroup (k_gemv_fold's way) meant 128 KB of input-layer
+// weights per CU, the longest phase of the launch (tools/trace_chain.py).  Its tile is layer 2's
+// residual too; later blocks read theirs from layer l - 2's hand-off.  Workgroup 0 (layer 1, tile
+// 0; idle once its tile is out) then runs the output layer on the last layer's hand-off
+// (p3d_gemv_fold_out) and advances the slot's epoch: every workgroup has read the epoch by then
+// (each published with its tag, and each layer's tiles were all gathered by the next layer's).
+// Every wait is bounded (err); the launch needs its grid resident (host: H L / 16 <= CUs).  Same
+// k_gemv arithmetic throughout, so the same bits as the six launches
+// (tests/test_gpu_parity.py::test_gemv_small_batch).
 #define P3D_GEMV_CHAIN_MAXH 8
 #define P3D_GEMV_CHAIN_MAXK 2048   // (L = 2048: the second half of each wave's slice requested after the first's FMAs)
 struct GemvChain {
@@ -432,7 +489,8 @@ struct GemvChain {
   GemvArgs out;                         // the output layer (Y = the user's y, row-major)
   int H, T;                             // hidden layers; column tiles per layer (L / 16)
   int res;                              // residual blocks: layer l even adds layer l - 2's output
-  float* hand;                          // this slot: [H][4 rows][L / 2] 16-B granules
+  float* hand;                          // this slot: [H + 1][4 rows][L / 2] 16-B granules (0: the input
+                                        // layer's output, l: hidden layer l's)
   unsigned* epoch;                      // this slot's epoch word (tag = epoch + 1)
   int* err;
 };
@@ -445,9 +503,15 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   constexpr int WV = 16;
   __shared__ float xs[MR * P3D_GEMV_CHAIN_MAXK];
   __shared__ float red[4][WV][MR][16];
-  __shared__ float xin[MR][P3D_GEMV_FOLD_MAXIN];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
+#ifdef P3D_TRACE   // development builds (tools/trace_chain.py): per workgroup at 8 b: start, input,
+                   // contracted, published; workgroup 0 also output gathered (4), end (5)
+#define P3D_CH_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 512) g_p3d_trace[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define P3D_CH_STAMP(k) do { } while (0)
+#endif
+  P3D_CH_STAMP(0);
   const unsigned tag = __hip_atomic_load(c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int b = blockIdx.x, l = 1 + b / c.T, t = b - (l - 1) * c.T;
   // this layer's arguments, read with constant indices only (a runtime index into the argument
@@ -462,46 +526,45 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   const __amdgpu_buffer_rsrc_t rh = p3d_rsrc(c.hand);
   const int gpl = 4 * (N >> 1);                  // granules per layer
   // ---- the weight slice, then the epilogue operands (wave 0, lane (i, q) = row q, column col) ---
-  // (layer 1: after the input layer -- its weights held across that phase would spill)
-  const f32x4* pw = (const f32x4*)p.Wf + (int64_t)t * ngK * 64 + lane;
-  f32x4 wf[GC];
-  if (l != 1) p3d_gemv_preload<GC>(pw, gb, ge, wf);
-  GemvEpi e;
-  e.ctr = p.ctr;
-  if (l != 1 && w == 0 && q < M) p3d_gemv_epi_load(p, q, col, e);
-  // ---- the residual tile (wave 0): layer 2 recomputes the input layer's, later layers read theirs
+  // ---- layer 2's wave 0 first computes the input layer's tile t (hand-off slot 0): layer 1's
+  // input, and layer 2's own residual when blocks are residual.  Before its weight slice: a wave's
+  // loads complete in issue order, so operands requested behind 4 KB of weights wait for them. ----
   const bool second = c.res && l >= 2 && (l & 1) == 0;
   float rv = 0.f;
+  if (l == 2 && w == 0) {
+    float v0 = 0.f;
+    if (q < M) {
+      f32x4 wv[2][4];
+      GemvEpi ei;
+      p3d_gemv_in_weights(c.in, col, wv);
+      p3d_gemv_epi_load(c.in, 0, col, ei);
+      v0 = p3d_gemv_in_value_g(c.in, wv, ei, q, col);
+    }
+    p3d_gemv_publish(rh, 0, M, N, col, v0, tag);
+    rv = v0;
+  }
+  const f32x4* pw = (const f32x4*)p.Wf + (int64_t)t * ngK * 64 + lane;
+  f32x4 wf[GC];
+  p3d_gemv_preload<GC>(pw, gb, ge, wf);
+  GemvEpi e;
+  e.ctr = p.ctr;
+  if (w == 0 && q < M) p3d_gemv_epi_load(p, q, col, e);
+  p3d_pin<GC>(wf);   // (every wait below is far longer than these loads)
+  p3d_pin_epi(e);
+  // ---- the residual tile of later blocks: layer l - 2's hand-off (wave 0) -----------------------
   if (second && l > 2 && w == 0 && q < M) {
-    const u32x4_t v0 = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-        rh, ((l - 3) * gpl + q * (N >> 1) + (col >> 1)) * 16, 0, 16));
-    u32x4_t v = v0;
+    const int off = ((l - 2) * gpl + q * (N >> 1) + (col >> 1)) * 16;
+    u32x4_t v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rh, off, 0, 16));
     for (int spin = 0; !(v.y == tag && v.w == tag); ++spin) {
       if (spin > P3D_XCHG_SPIN) { __hip_atomic_store(c.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
       __builtin_amdgcn_s_sleep(1);
-      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-          rh, ((l - 3) * gpl + q * (N >> 1) + (col >> 1)) * 16, 0, 16));
+      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rh, off, 0, 16));
     }
     rv = __uint_as_float((i & 1) ? v.z : v.x);
   }
-  // ---- this layer's input --------------------------------------------------------------------
-  if (l == 1) {
-    GemvArgs in = c.in;
-    in.Y = nullptr;
-    p3d_gemv_fold_in<MR, 64 * WV>(in, -1, xs, xin);
-    p3d_gemv_preload<GC>(pw, gb, ge, wf);
-    if (w == 0 && q < M) p3d_gemv_epi_load(p, q, col, e);
-  } else {
-    if (second && l == 2) {
-      p3d_gemv_stage_x<64 * WV>(c.in, xin);
-      if (w == 0 && q < M) {
-        f32x4 wv[2][4];
-        p3d_gemv_in_weights(c.in, col, wv);
-        rv = p3d_gemv_in_value(c.in, xin, wv, q, col);
-      }
-    }
-    p3d_gemv_gather<64 * WV>(rh, (l - 2) * gpl, M, K, tag, xs, c.err);
-  }
+  // ---- this layer's input: layer l - 1's hand-off (slot 0: the input layer) --------------------
+  p3d_gemv_gather<64 * WV>(rh, (l - 1) * gpl, M, K, tag, xs, c.err);
+  P3D_CH_STAMP(1);
   // ---- contraction, quarters, waves (k_gemv) -------------------------------------------------
   float acc[MR];
 #pragma unroll
@@ -518,21 +581,27 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
     for (int r = 0; r < MR; ++r) red[0][w][r][i] = acc[r];
   }
   __syncthreads();
+  P3D_CH_STAMP(2);
   if (w == 0) {
     float zs = 0.f;
 #pragma unroll
     for (int u = 0; u < WV; ++u) zs += red[0][u][q][i];
     float y = p3d_gemv_epi(p, e, zs, q, col);   // (p.res is null: the residual is added last, as there)
     if (second) y += rv;
-    p3d_gemv_publish(rh, (l - 1) * gpl, M, N, col, y, tag);
+    p3d_gemv_publish(rh, l * gpl, M, N, col, y, tag);
+#ifdef P3D_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    P3D_CH_STAMP(3);
   }
   if (b != 0) return;
   // ---- workgroup 0: the output layer on the last layer's hand-off -------------------------------
   GemvFold f{};
   f.fout = 1;
   f.out = c.out;
-  f.hand = c.hand + (int64_t)(c.H - 1) * gpl * 4;
+  f.hand = c.hand + (int64_t)c.H * gpl * 4;
   f.epoch = c.epoch;
   f.err = c.err;
   p3d_gemv_fold_out<MR, WV, 4>(f, tag, xs, red);
+  P3D_CH_STAMP(5);
 }
