@@ -2516,7 +2516,8 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
     LAUNCH_CHECK("k_gemm_bf16s");
     return P3D_OK;
   }
-  if (l > 0) m->bf16_kname = m->bf16_stages == 48 ? "k_gemm_bf16p<64, 4, 8, false>" : "k_gemm_bf16p";
+  if (l > 0) m->bf16_kname = m->bf16_stages == 48 ? "k_gemm_bf16p<64, 4, 8, false>"
+                             : (m->bf16_stages == 99 && ly.K % 256 == 0) ? "k_gemm_bf16r<64, 4>" : "k_gemm_bf16p";
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
     if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
@@ -2525,6 +2526,7 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
     else if (m->bf16_stages == 22) go(ps, k_gemm_bf16p<128, 2, 4>, dim3(grid), dim3(256), st, a);
     else if (m->bf16_stages == 38) go(ps, k_gemm_bf16p<64, 3, 8>, dim3(grid), dim3(512), st, a);
     else if (m->bf16_stages == 28) go(ps, k_gemm_bf16p<128, 2, 8>, dim3(grid), dim3(512), st, a);
+    else if (m->bf16_stages == 99 && ly.K % 256 == 0) go(ps, k_gemm_bf16r<64, 4>, dim3(grid), dim3(512), st, a);
     else if (m->bf16_stages == 48) go(ps, k_gemm_bf16p<64, 4, 8>, dim3(grid), dim3(512), st, a);
     else if (m->bf16_stages == 49) go(ps, k_gemm_bf16p<64, 4, 8, true>, dim3(grid), dim3(512), st, a);
     else if (m->bf16_stages == 39) go(ps, k_gemm_bf16p<64, 3, 8, true>, dim3(grid), dim3(512), st, a);
