@@ -87,6 +87,8 @@ SIGNATURES = [
                                 c_int32, c_void_p]),
     ("p3d_unnormalize", c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                   c_void_p, c_void_p]),
+    ("p3d_lift", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                           c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     ("p3d_moments_workspace", c_int64, [c_int64, c_int32]),
     ("p3d_moments", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_crc32c", c_uint32, [c_void_p, c_int64, c_uint32]),

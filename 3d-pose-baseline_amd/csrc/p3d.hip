@@ -1697,6 +1697,8 @@ struct p3d_model {
   int gemv_slots = 0;       // workspace slots (ws_row / 16) the fold's hand-off buffer covers (others unfolded)
   int64_t gemv_slot_floats = 0;     // hand-off floats per slot (the chain's H layers, or the fold's one)
   float* gemv_hand = nullptr;       // [slot][layers][4 rows][L / 2] 16-B granules (layer-output hand-offs)
+  float* lift_x = nullptr;          // p3d_lift's normalised rows and outputs where it runs the three steps
+  float* lift_y = nullptr;
   unsigned* gemv_epoch = nullptr;   // [slot] epoch words, P3D_XCHG_EPOCH_STRIDE apart
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
@@ -1815,6 +1817,8 @@ void free_all(p3d_model* m) {
   if (m->bf16s_sync) (void)hipFree(m->bf16s_sync);
   if (m->xsync) (void)hipFree(m->xsync);
   if (m->gemv_hand) (void)hipFree(m->gemv_hand);
+  if (m->lift_x) (void)hipFree(m->lift_x);
+  if (m->lift_y) (void)hipFree(m->lift_y);
   if (m->gemv_epoch) (void)hipFree(m->gemv_epoch);
   if (m->errw) (void)hipHostFree(m->errw);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
@@ -2079,6 +2083,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
       const int64_t nh = (int64_t)m->gemv_slots * m->gemv_slot_floats;
       if ((e = hipMalloc(&m->gemv_hand, nh * sizeof(float))) != hipSuccess) return cleanup(e);
       if ((e = hipMemset(m->gemv_hand, 0, nh * sizeof(float))) != hipSuccess) return cleanup(e);
+      if ((e = hipMalloc(&m->lift_x, (size_t)c.max_batch * c.input_size * sizeof(float))) != hipSuccess) return cleanup(e);
+      if ((e = hipMalloc(&m->lift_y, (size_t)c.max_batch * c.output_size * sizeof(float))) != hipSuccess) return cleanup(e);
       const int64_t ne = (int64_t)m->gemv_slots * P3D_XCHG_EPOCH_STRIDE;
       if ((e = hipMalloc(&m->gemv_epoch, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
       if ((e = hipMemset(m->gemv_epoch, 0, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
@@ -2573,8 +2579,11 @@ static int forward_bf16(p3d_model* m, const float* x, int64_t B, float* y, hipSt
 // Batch <= 4 inference (p3d_gemv.h): every layer as one weight-streaming k_gemv launch, the input
 // and output layers folded into the first / last hidden layer's launch (k_gemv_fold) where the
 // workspace slot has a hand-off area -- four launches instead of six at num_layers = 2, same bits.
+// fr (p3d_lift): the chain reads the raw rows and writes the unnormalised ones; returns 1 without
+// launching anything where the chain does not run (the caller then takes the three steps).
 static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float keep_prob, uint64_t seed,
-                        uint64_t ctr, int64_t row_offset, int64_t ws_row, hipStream_t st) {
+                        uint64_t ctr, int64_t row_offset, int64_t ws_row, hipStream_t st,
+                        const GemvFrames* fr = nullptr) {
   const p3d_cfg& c = m->cfg;
   const int nl = (int)m->layers.size();
   const int64_t wsoff = (ws_row >> 4) * (int64_t)(c.linear_size >> 4) * 256;  // packed row-tile offset
@@ -2623,6 +2632,7 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
     ch.hand = m->gemv_hand + slot * m->gemv_slot_floats;
     ch.epoch = m->gemv_epoch + slot * P3D_XCHG_EPOCH_STRIDE;
     ch.err = m->xerr;
+    if (fr) { ch.fr = *fr; ch.out.Y = nullptr; }
     {
       ProfScope ps(m, "gemv_chain");
       go(ps, k_gemv_chain<4, 4>, dim3((unsigned)(H * T)), dim3(1024), st, ch);
@@ -2630,6 +2640,7 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
     LAUNCH_CHECK("k_gemv_chain");
     return P3D_OK;
   }
+  if (fr) return 1;
   const float* in = x;
   for (int l = 0; l < nl; ++l) {
     const bool last = (l == nl - 1);
@@ -3949,6 +3960,35 @@ extern "C" int p3d_unnormalize(const void* xn, int32_t in_dtype, int64_t F, int3
   else k_unnormalize<false><<<grid, 256, 0, (hipStream_t)stream>>>(xn, F, U, mean, stdv, dims_to_use, D, out);
   LAUNCH_CHECK("k_unnormalize");
   return 0;
+}
+
+// src/openpose_3dpose_sandbox.py:347-356 per call: normalise the mapped 2D rows (float32, the
+// placeholder cast), the eval forward, unNormalizeData -- as ONE launch where the batch-1 chain
+// runs (B <= 4, the model's hidden layers on the device at once), else as p3d_normalize +
+// p3d_forward_ex + p3d_unnormalize; the same bits either way.
+extern "C" int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, const double* mean2,
+                        const double* std2, const int32_t* use2, int32_t U2, const double* mean3, const double* std3,
+                        const int32_t* use3, int32_t U3, int32_t D3, double* out, void* stream) {
+  if (!m || !raw || !mean2 || !std2 || !use2 || !mean3 || !std3 || !use3 || !out)
+    return fail(P3D_ERR_ARG, "p3d_lift: null argument");
+  const p3d_cfg& c = m->cfg;
+  if (B <= 0 || B > c.max_batch) return fail(P3D_ERR_ARG, "p3d_lift: batch must be in 1..max_batch");
+  if (U2 != c.input_size || U3 != c.output_size || D2 < U2 || D3 < U3 || D3 > 256)
+    return fail(P3D_ERR_ARG, "p3d_lift: dimension sets do not match the model");
+  if (c.dtype != P3D_DTYPE_F32 || !m->lift_x) return fail(P3D_ERR_ARG, "p3d_lift: float32 models with the batch<=4 path");
+  hipStream_t st = (hipStream_t)stream;
+  if (B <= m->gemv_maxb) {
+    GemvFrames fr{};
+    fr.raw = raw; fr.ldraw = D2; fr.mean2 = mean2; fr.std2 = std2; fr.use2 = use2;
+    fr.out = out; fr.D3 = D3; fr.mean3 = mean3; fr.std3 = std3; fr.use3 = use3;
+    const int r = forward_gemv(m, nullptr, B, nullptr, 1.0f, 0, 0, 0, 0, st, &fr);   // (keep 1: no dropout, seed unused)
+    if (r != 1) return r;
+  }
+  int r = p3d_normalize(raw, B, D2, mean2, std2, use2, U2, m->lift_x, P3D_DTYPE_F32, stream);
+  if (r) return r;
+  r = forward_impl(m, m->lift_x, B, m->lift_y, 0, 1.0f, 0, 0, 0, 0, stream, nullptr);
+  if (r) return r;
+  return p3d_unnormalize(m->lift_y, P3D_DTYPE_F32, B, U3, mean3, std3, use3, D3, out, stream);
 }
 
 extern "C" int64_t p3d_moments_workspace(int64_t F, int32_t D) {

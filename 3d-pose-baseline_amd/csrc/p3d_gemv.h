@@ -52,6 +52,14 @@ struct GemvArgs {
   float* Y; int64_t ldy; int ypk;         // packed (hidden) or row-major (output layer)
 };
 
+// Frame I/O of p3d_lift: the raw 2D rows in, the unNormalizeData'd 3D rows out.
+struct GemvFrames {
+  const double* raw; int ldraw;                                      // [M][ldraw] float64 (null: off)
+  const double* mean2; const double* std2; const int32_t* use2;      // use2: in.K columns of raw
+  double* out; int D3;                                               // [M][D3] float64 (null: off)
+  const double* mean3; const double* std3; const int32_t* use3;      // use3: out.N columns of out
+};
+
 // ---- the layer epilogue of k_fwd for one (row, column) ---------------------------------------
 struct GemvEpi {
   float b = 0.f, gam = 1.f, bet = 0.f, mmu = 0.f, mva = 1.f, rv = 0.f, mxv = 1.f;
@@ -196,6 +204,7 @@ struct GemvFold {
   float* hand;        // this workspace slot's hand-off: [4 rows][N / 2] 16-B granules {a, tag, b, tag}
   unsigned* epoch;    // this slot's epoch word (tag = epoch + 1), advanced by the consumer
   int* err;           // host-visible error word: 1 = the consumer's spin ran out
+  GemvFrames fr;      // p3d_lift's output side (fr.out null: off)
 };
 
 // The input layer (K = 32) for feature f of row r, as k_gemv<MR, 2, GC> computes it (wave w of
@@ -211,6 +220,43 @@ __device__ __forceinline__ float p3d_gemv_in_value(const GemvArgs& in, const flo
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4 xv = *(const f32x4*)&xin[r][16 * g + 4 * q];
+      float s = 0.f;
+      s = fmaf(wv[g][q].x, xv.x, s);
+      s = fmaf(wv[g][q].y, xv.y, s);
+      s = fmaf(wv[g][q].z, xv.z, s);
+      s = fmaf(wv[g][q].w, xv.w, s);
+      a[q] = s;
+    }
+    const float t = (a[0] + a[1]) + (a[2] + a[3]);
+    zs += t;
+  }
+  return p3d_gemv_epi(in, e, zs, r, f);
+}
+// p3d_normalize's and p3d_unnormalize's element expressions (csrc/p3d_data.h, contraction off)
+__device__ __forceinline__ float p3d_norm_in(double x, double mu, double sd) {
+#pragma clang fp contract(off)
+  return (float)((x - mu) / sd);
+}
+__device__ __forceinline__ double p3d_unnorm_out(float v, double sd, double mu) {
+#pragma clang fp contract(off)
+  return (double)v * sd + mu;
+}
+// the input layer's value from the raw rows, normalised as p3d_normalize rounds them to float32
+__device__ __forceinline__ float p3d_gemv_in_value_n(const GemvArgs& in, const GemvFrames& fr, const f32x4 (&wv)[2][4],
+                                                     const GemvEpi& e, int r, int f) {
+  const double* xr = fr.raw + (int64_t)r * fr.ldraw;
+  float zs = 0.f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 xv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = fr.use2[16 * g + 4 * q + k];
+        xv[k] = p3d_norm_in(xr[d], fr.mean2[d], fr.std2[d]);
+      }
       float s = 0.f;
       s = fmaf(wv[g][q].x, xv.x, s);
       s = fmaf(wv[g][q].y, xv.y, s);
@@ -388,6 +434,15 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     }
   }
   __syncthreads();
+  if (f.fr.out && w != 0) {
+    // unNormalizeData's unused dimensions: (float) 0 * std + mean (waves 1.., beside wave 0)
+    for (int k = (int)threadIdx.x - 64; k < M * f.fr.D3; k += 64 * (WV - 1)) {
+      const int r = k / f.fr.D3, d = k - r * f.fr.D3;
+      bool used = false;
+      for (int u = 0; u < o.N; ++u) used |= f.fr.use3[u] == d;
+      if (!used) f.fr.out[(int64_t)r * f.fr.D3 + d] = p3d_unnorm_out(0.0f, f.fr.std3[d], f.fr.mean3[d]);
+    }
+  }
   if (w != 0 || q >= M || q >= MR) return;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -397,7 +452,13 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
 #pragma unroll
     for (int u = 0; u < WV; ++u) zs += red[t][u][q][i];
     const float y = p3d_gemv_epi(o, e[t], zs, q, col < o.N ? col : o.N - 1);
-    if (col < o.N) o.Y[(int64_t)q * o.ldy + col] = y;
+    if (col < o.N) {
+      if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
+      if (f.fr.out) {
+        const int d = f.fr.use3[col];
+        f.fr.out[(int64_t)q * f.fr.D3 + d] = p3d_unnorm_out(y, f.fr.std3[d], f.fr.mean3[d]);
+      }
+    }
   }
 }
 
@@ -493,6 +554,7 @@ struct GemvChain {
                                         // layer's output, l: hidden layer l's)
   unsigned* epoch;                      // this slot's epoch word (tag = epoch + 1)
   int* err;
+  GemvFrames fr;                        // p3d_lift: raw 2D rows in (fr.raw), 3D rows out (fr.out)
 };
 
 // (Measured and rejected: each wave DMAing its fragments into LDS at kernel start -- layer 1 too,
@@ -538,7 +600,7 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
       GemvEpi ei;
       p3d_gemv_in_weights(c.in, col, wv);
       p3d_gemv_epi_load(c.in, 0, col, ei);
-      v0 = p3d_gemv_in_value_g(c.in, wv, ei, q, col);
+      v0 = c.fr.raw ? p3d_gemv_in_value_n(c.in, c.fr, wv, ei, q, col) : p3d_gemv_in_value_g(c.in, wv, ei, q, col);
     }
     p3d_gemv_publish(rh, 0, M, N, col, v0, tag);
     rv = v0;
@@ -602,6 +664,7 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   f.hand = c.hand + (int64_t)c.H * gpl * 4;
   f.epoch = c.epoch;
   f.err = c.err;
+  f.fr = c.fr;
   p3d_gemv_fold_out<MR, WV, 4>(f, tag, xs, red);
   P3D_CH_STAMP(5);
 }

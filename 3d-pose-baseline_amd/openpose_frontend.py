@@ -6,8 +6,9 @@ the 64-wide H3.6M 2D vector (``order`` of :25 plus the derived Hip / Neck-Nose /
 (:353) and ``unNormalizeData`` of the 3D output (:356).
 
 ``FrameLifter`` runs everything after the joint mapping as ONE HIP graph per call: pinned H2D
-of the mapped frame(s) -> ``p3d_normalize`` (float32, the placeholder cast) -> the six layer
-kernels -> ``p3d_unnormalize`` -> pinned D2H of the [B, 96] millimetre pose(s).  The mapping is
+of the mapped frame(s) -> ``p3d_lift`` (normalise, the float32 placeholder cast, the forward,
+unNormalizeData: one persistent launch at batch <= 4, else ``p3d_normalize`` + the layer kernels +
+``p3d_unnormalize``, the same bits) -> pinned D2H of the [B, 96] millimetre pose(s).  The mapping is
 a host-side index shuffle of the OpenPose JSON values (as in the reference).  The plotting,
 axis swap and Maya export that follow in the sandbox are out of scope.
 """
@@ -34,6 +35,18 @@ def map_frames(frames_xy):
     e[:, 28:30] = (e[:, 30:32] + e[:, 24:26]) / 2        # Neck/Nose = mean(Head, Spine)
     e[:, 26:28] = 2 * e[:, 24:26] - e[:, 28:30]          # Thorax = 2 Spine - Neck/Nose
     return e
+
+
+def lift(model, raw, mean2, std2, use2, mean3, std3, use3, out):
+    """Device rows raw [B, 64] float64 (mapped frames) -> out [B, D3] float64 millimetres:
+    normalize_data, the float32 cast, the eval forward, unNormalizeData (p3d_lift).  mean/std:
+    device float64; use2/use3: device int32 dimension sets (data_pipeline._dims)."""
+    import _p3d
+    p = lambda t: t.data_ptr()   # noqa: E731
+    _p3d.check(_p3d.lib().p3d_lift(model._h, p(raw), raw.shape[0], raw.shape[1], p(mean2), p(std2), p(use2),
+                                   use2.numel(), p(mean3), p(std3), p(use3), use3.numel(), out.shape[1], p(out),
+                                   model.stream()), "p3d_lift")
+    return out
 
 
 class FrameLifter:
@@ -76,9 +89,7 @@ class FrameLifter:
 
     def _body(self):
         self.din.copy_(self.hin, non_blocking=True)
-        dp.normalize(self.din, self.m2, self.s2, self.u2, out_dtype=self.torch.float32, out=self.x)
-        self.model.forward_device(self.x, False, 1.0, out=self.y, ctr=0)
-        dp.unnormalize(self.y, self.m3, self.s3, self.u3, self.p3.shape[1], out=self.p3)
+        lift(self.model, self.din, self.m2, self.s2, self.u2, self.m3, self.s3, self.u3, out=self.p3)
         self.hout.copy_(self.p3, non_blocking=True)
 
     def lift_mapped(self, enc_in64):

@@ -357,6 +357,15 @@ int p3d_unnormalize(const void* xn, int32_t in_dtype, int64_t F, int32_t U, cons
                     const double* stdv, const int32_t* dims_to_use, int32_t D, double* out,
                     void* stream);
 
+/* src/openpose_3dpose_sandbox.py:347-356 per call (normalize_data of the mapped 2D rows, the
+ * float32 placeholder cast, model.step at is_training False / keep 1, unNormalizeData): raw
+ * [B, D2] float64 -> out [B, D3] float64.  U2 / U3 must equal the model's input / output size.
+ * One launch where the batch <= 4 persistent chain runs, else p3d_normalize + p3d_forward_ex +
+ * p3d_unnormalize; the same bits as those three calls either way.  Float32 models. */
+int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, const double* mean2, const double* std2,
+             const int32_t* use2, int32_t U2, const double* mean3, const double* std3, const int32_t* use3,
+             int32_t U3, int32_t D3, double* out, void* stream);
+
 /* np.mean / np.std (population) over axis 0 of x [F, D], D <= 256 -- the statistics of
  * src/data_utils.py:210-211 (normalization_stats).  Deterministic two-level column sums;
  * `work` must hold p3d_moments_workspace(F, D) bytes of device memory. */

@@ -68,3 +68,28 @@ def test_frame_lifter_rejects_bad_input():
     with pytest.raises(ValueError):
         of.FrameLifter(m, s["mean2"], s["std2"], use2[:10], s["mean3"], s["std3"], ign3)
     m.close()
+
+
+@pytest.mark.parametrize("B", [1, 3, 4, 8])
+def test_lift_bit_identical_to_three_steps(B, monkeypatch):
+    """p3d_lift (normalise + forward + unNormalizeData; one persistent launch at B <= 4) == the
+    three calls p3d_normalize (float32) -> forward -> p3d_unnormalize, bit for bit; and with the
+    chain off (P3D_GEMV_CHAIN=0: p3d_lift takes the three steps itself)."""
+    import data_pipeline as dp
+    outs = []
+    for chain in ("1", "0"):
+        monkeypatch.setenv("P3D_GEMV_CHAIN", chain)
+        st, m, s, use2, use3, ign3, frames = setup()
+        e = torch.from_numpy(of.map_frames(frames[:B])).cuda()
+        m2, s2, m3, s3 = (dp.as_device(s[k]) for k in ("mean2", "std2", "mean3", "std3"))
+        u2, u3 = dp._dims(use2, 64, "t"), dp._dims(use3, 96, "t")
+        out = torch.empty((B, 96), dtype=torch.float64, device="cuda")
+        of.lift(m, e, m2, s2, u2, m3, s3, u3, out=out)
+        x = dp.normalize(e, m2, s2, u2, out_dtype=torch.float32)
+        y = m.forward_device(x, False, 1.0, ctr=0)
+        ref = dp.unnormalize(y, m3, s3, u3, 96)
+        assert torch.equal(out, ref), (chain, (out - ref).abs().max().item())
+        m.check_errors()
+        outs.append(out.cpu())
+        m.close()
+    assert torch.equal(outs[0], outs[1])
