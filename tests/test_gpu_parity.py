@@ -630,6 +630,8 @@ def test_bf16_inference_matches_emulated_oracle(L, N, B):
     m.close()
 
 
+@pytest.mark.skipif(os.environ.get("P3D_TEST_BF16R") != "1",
+                    reason="opt-in kernel (P3D_BF16_STAGES=99) not yet validated on the box")
 @pytest.mark.parametrize("L,N,B", [(4096, 4, 1024), (512, 1, 200), (256, 2, 128)])
 def test_bf16_register_b_bit_identical(L, N, B, monkeypatch):
     """k_gemm_bf16r (A on the LDS-DMA ring, B loaded straight into registers, p3d_bf16.h) ==
