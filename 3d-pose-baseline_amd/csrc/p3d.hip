@@ -1619,9 +1619,9 @@ struct p3d_model {
   int train_split = 1;        // BN-train layers as GEMM (256 WGs) + k_bn_fwd / k_bn_bwd (env P3D_TRAIN_SPLIT)
   int in_train_wk = 2;        // waves of the BN-train input-layer launch (exchange form; env P3D_IN_TRAIN_WK: 8, 4, 2)
   int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
-  int xchg_wk = 8;            // BN-train hidden exchange-form forward tiling (env P3D_XCHG_WK: 8 = 8 waves
-                              // with an 8-deep ring; 16 (16 waves, measured 8.6 vs 6.8 us), 84, 82: ring 4, 2)
-  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8, 162 = 16 with a 2-deep ring)
+  int xchg_wk = 8;            // BN-train hidden exchange-form forward: 8 waves with an 8-deep ring (measured and
+                              // pruned in round 4: 16 waves 8.6 vs 6.8 us; rings of 4 / 2 within 1 %)
+  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -1640,7 +1640,7 @@ struct p3d_model {
   float* aff = nullptr;             // BN-eval affine per BN layer
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
-  int bf16_stages = 48;             // hidden bf16 GEMM variant (launch_bf16_layer; env P3D_BF16_STAGES)
+  int bf16_stages = 48;             // hidden bf16 GEMM form (launch_bf16_layer; env P3D_BF16_STAGES: 48, 99, 0)
   int bf16_split = 0;               // hidden bf16 layers as k_gemm_bf16s (256 x 128 tiles, K split in two
                                     // halves that meet in the launch) where M % 256 == 0 (env P3D_BF16_SPLIT=1;
                                     // measured 43.9 vs 44.6 us in step order, 42.5 vs 39.0 us hot: opt-in)
@@ -2061,7 +2061,6 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_IN_TRAIN_WK")) m->in_train_wk = atoi(ev);
   if (const char* ev = getenv("P3D_DGRAD_OUT_WK")) m->dgrad_out_wk = atoi(ev);
-  if (const char* ev = getenv("P3D_XCHG_WK")) m->xchg_wk = atoi(ev);
   if (const char* ev = getenv("P3D_DGRAD_WK")) m->dgrad_wk = atoi(ev);
   if (const char* ev = getenv("P3D_TRAIN_XCHG")) m->train_xchg = atoi(ev);
   {
@@ -2388,9 +2387,6 @@ static int launch_fwd_split(p3d_model* m, const FwdArgs& a0, int kind, hipStream
     if (kind == 0 && m->in_train_wk == 2 && a.K <= 32) go(ps, k_fwd<1, 2, 1, 2, false, true, 0>, g, dim3(128), st, a);
     else if (kind == 0 && m->in_train_wk == 4 && a.K <= 64) go(ps, k_fwd<1, 4, 1, 2, false, true, 0>, g, dim3(256), st, a);
     else if (kind == 0) go(ps, k_fwd<1, 8, 8, 2, false, true, 0>, g, dim3(512), st, a);
-    else if (m->xchg_wk == 16) go(ps, k_fwd<1, 16, 4, 2, true, true, 1>, g, dim3(1024), st, a);
-    else if (m->xchg_wk == 84) go(ps, k_fwd<1, 8, 4, 2, true, true, 1>, g, dim3(512), st, a);
-    else if (m->xchg_wk == 82) go(ps, k_fwd<1, 8, 2, 2, true, true, 1>, g, dim3(512), st, a);
     else go(ps, k_fwd<1, 8, 8, 2, true, true, 1>, g, dim3(512), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
@@ -2522,23 +2518,16 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
     LAUNCH_CHECK("k_gemm_bf16s");
     return P3D_OK;
   }
-  if (l > 0) m->bf16_kname = m->bf16_stages == 48 ? "k_gemm_bf16p<64, 4, 8, false>"
-                             : (m->bf16_stages == 99 && ly.K % 256 == 0) ? "k_gemm_bf16r<64, 4>" : "k_gemm_bf16p";
+  // hidden layers: k_gemm_bf16p<64, 4, 8> (default), k_gemm_bf16r<64, 4> (P3D_BF16_STAGES=99, K a
+  // multiple of 256), the unpipelined k_gemm_bf16<64, 4> (P3D_BF16_STAGES=0, reference form)
+  const bool breg = m->bf16_stages == 99 && ly.K % 256 == 0, bplain = m->bf16_stages == 0;
+  if (l > 0) m->bf16_kname = breg ? "k_gemm_bf16r<64, 4>" : bplain ? "k_gemm_bf16<64, 4>" : "k_gemm_bf16p<64, 4, 8, false>";
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
     if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
-    else if (m->bf16_stages == 32) go(ps, k_gemm_bf16p<64, 3, 4>, dim3(grid), dim3(256), st, a);
-    else if (m->bf16_stages == 42) go(ps, k_gemm_bf16p<64, 4, 4>, dim3(grid), dim3(256), st, a);
-    else if (m->bf16_stages == 22) go(ps, k_gemm_bf16p<128, 2, 4>, dim3(grid), dim3(256), st, a);
-    else if (m->bf16_stages == 38) go(ps, k_gemm_bf16p<64, 3, 8>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 28) go(ps, k_gemm_bf16p<128, 2, 8>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 99 && ly.K % 256 == 0) go(ps, k_gemm_bf16r<64, 4>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 48) go(ps, k_gemm_bf16p<64, 4, 8>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 49) go(ps, k_gemm_bf16p<64, 4, 8, true>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 39) go(ps, k_gemm_bf16p<64, 3, 8, true>, dim3(grid), dim3(512), st, a);
-    else if (m->bf16_stages == 2) go(ps, k_gemm_bf16<64, 2>, dim3(grid), dim3(256), st, a);
-    else if (m->bf16_stages == 3) go(ps, k_gemm_bf16<64, 3>, dim3(grid), dim3(256), st, a);
-    else go(ps, k_gemm_bf16<64, 4>, dim3(grid), dim3(256), st, a);
+    else if (breg) go(ps, k_gemm_bf16r<64, 4>, dim3(grid), dim3(512), st, a);
+    else if (bplain) go(ps, k_gemm_bf16<64, 4>, dim3(grid), dim3(256), st, a);
+    else go(ps, k_gemm_bf16p<64, 4, 8>, dim3(grid), dim3(512), st, a);
   }
   LAUNCH_CHECK("k_gemm_bf16");
   return P3D_OK;
@@ -3391,7 +3380,6 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           // 16 waves (both BN forms, so they keep giving the same bits): 6.8 vs 7.0-7.1 us per
           // hidden dgrad (A/B, one box); the attached-wgrad form keeps k_dgrad_wg's 8-wave split
           if (m->dgrad_wk == 16 && !m->wgrad_attach) go(ps, k_dgrad<1, 16, 4, 2, true, 1>, g, dim3(1024), st, a);
-          else if (m->dgrad_wk == 162 && !m->wgrad_attach) go(ps, k_dgrad<1, 16, 2, 2, true, 1>, g, dim3(1024), st, a);
           else go(ps, k_dgrad<1, 8, 8, 2, true, 1>, g, dim3(512), st, a);
         } else {
           dim3 g = grid;
