@@ -1640,7 +1640,7 @@ struct p3d_model {
   float* aff = nullptr;             // BN-eval affine per BN layer
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
-  int bf16_stages = 48;             // hidden bf16 GEMM form (launch_bf16_layer; env P3D_BF16_STAGES: 48, 99, 0)
+  int bf16_stages = 48;             // hidden bf16 GEMM form (launch_bf16_layer; env P3D_BF16_STAGES: 48, 0)
   int bf16_split = 0;               // hidden bf16 layers as k_gemm_bf16s (256 x 128 tiles, K split in two
                                     // halves that meet in the launch) where M % 256 == 0 (env P3D_BF16_SPLIT=1;
                                     // measured 43.9 vs 44.6 us in step order, 42.5 vs 39.0 us hot: opt-in)
@@ -2518,14 +2518,13 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
     LAUNCH_CHECK("k_gemm_bf16s");
     return P3D_OK;
   }
-  // hidden layers: k_gemm_bf16p<64, 4, 8> (default), k_gemm_bf16r<64, 4> (P3D_BF16_STAGES=99, K a
-  // multiple of 256), the unpipelined k_gemm_bf16<64, 4> (P3D_BF16_STAGES=0, reference form)
-  const bool breg = m->bf16_stages == 99 && ly.K % 256 == 0, bplain = m->bf16_stages == 0;
-  if (l > 0) m->bf16_kname = breg ? "k_gemm_bf16r<64, 4>" : bplain ? "k_gemm_bf16<64, 4>" : "k_gemm_bf16p<64, 4, 8, false>";
+  // hidden layers: k_gemm_bf16p<64, 4, 8> (default), the unpipelined k_gemm_bf16<64, 4>
+  // (P3D_BF16_STAGES=0, reference form)
+  const bool bplain = m->bf16_stages == 0;
+  if (l > 0) m->bf16_kname = bplain ? "k_gemm_bf16<64, 4>" : "k_gemm_bf16p<64, 4, 8, false>";
   {
     ProfScope ps(m, l == 0 ? "bf16_in" : "bf16_hidden");
     if (l == 0) go(ps, k_gemm_bf16<32, 2>, dim3(grid), dim3(256), st, a);
-    else if (breg) go(ps, k_gemm_bf16r<64, 4>, dim3(grid), dim3(512), st, a);
     else if (bplain) go(ps, k_gemm_bf16<64, 4>, dim3(grid), dim3(256), st, a);
     else go(ps, k_gemm_bf16p<64, 4, 8>, dim3(grid), dim3(512), st, a);
   }

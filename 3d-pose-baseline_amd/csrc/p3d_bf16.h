@@ -345,150 +345,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_gemm_bf16p(GemmBf16Args p) {
   }
 }
 
-// B through registers (round 4): the same 128 x 128 tiles, 8 waves of 64 x 32 and epilogue as
-// k_gemm_bf16p<64, 4, 8>, but only the A operand rides the LDS-DMA ring (16 of the 32 KB per
-// 64-deep stage: one copy per CU, read by the four waves of its row half); each wave loads its own
-// two B column tiles straight into registers, NST - 1 stages ahead, beside the DMA.  The ablations
-// of section 5f put k_gemm_bf16p at its LDS-DMA intake (~65 GB/s per CU: 31 us of the 39 with no
-// MFMA at all); here that path carries half the bytes and B's 2 x 16 KB per stage (two waves per
-// column pair) come over the L2 -> VGPR path.  The B loads are inline asm: hipcc waits vmcnt(0)
-// at the first use of an ordinary load while an LDS-DMA is in flight; the stage waits count them
-// instead (PER = A DMAs + B loads per wave and stage), and a sched_barrier after each wait keeps
-// the MFMAs behind it.  The MFMAs run in k_gemm_bf16p's order: the same bits.
-__device__ __forceinline__ bf16x8 p3d_gload16(const unsigned char* ptr) {
-  bf16x8 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
-  return v;
-}
-template <int BK, int NST>
-__global__ __launch_bounds__(512) void k_gemm_bf16r(GemmBf16Args p) {
-  constexpr int WAVES = 8, KG = BK / 32, CT = 2, WN = 4;
-  constexpr int STAGE = 8 * KG * 1024;                 // A tiles only
-  constexpr int EPI = 128 * 132 * 4;
-  constexpr int LDS = (NST * STAGE > EPI) ? NST * STAGE : EPI;
-  constexpr int PERA = 8 * KG / WAVES;                 // A LDS-DMA instructions per wave and stage
-  constexpr int PER = PERA + CT * KG;                  // vector memory instructions per wave and stage
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w / WN, wn = w % WN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tiles_n = p.N / 128, tiles_m = p.M / 128;
-  const int GM = (tiles_m % 4 == 0) ? 4 : ((tiles_m % 2 == 0) ? 2 : 1);
-  const int grp = tile_id / (GM * tiles_n), in_grp = tile_id % (GM * tiles_n);
-  const int mt = grp * GM + (in_grp % GM), nt = in_grp / GM;
-  const int ngA = p.K / 32;
-  const int nks = p.K / BK;                            // a multiple of NST (host)
-  const unsigned char* Ag = (const unsigned char*)p.A + (int64_t)(8 * mt) * ngA * 1024;
-  const unsigned char* Bw = (const unsigned char*)p.Bt + ((int64_t)(8 * nt + CT * wn) * ngA) * 1024 + lane * 16;
-
-  auto issue = [&](int ks, int buf, bf16x8 (&rb)[KG][CT]) {
-    unsigned char* base = smem + buf * STAGE;
-#pragma unroll
-    for (int c = 0; c < PERA; ++c) {
-      const int t = w * PERA + c, j = t / KG, g = t % KG;
-      const unsigned char* src = Ag + ((int64_t)j * ngA + ks * KG + g) * 1024 + lane * 16;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + t * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int c = 0; c < CT; ++c) rb[g][c] = p3d_gload16(Bw + ((int64_t)c * ngA + ks * KG + g) * 1024);
-  };
-  auto readA = [&](int buf, int g, bf16x8 (&af)[4]) {
-    const unsigned char* base = smem + buf * STAGE;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) af[r] = *(const bf16x8*)(base + ((4 * wm + r) * KG + g) * 1024 + lane * 16);
-  };
-
-  f32x4 acc[4][CT];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < CT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[2][4];
-  bf16x8 rb[NST][KG][CT];
-
-#pragma unroll
-  for (int s0 = 0; s0 < NST - 1; ++s0)
-    if (s0 < nks) issue(s0, s0, rb[s0]);
-  {
-    const int later = (nks - 1) < (NST - 2) ? (nks - 1) : (NST - 2);
-    p3d_wait_stages<PER, NST>(later);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    readA(0, 0, fa[0]);
-  }
-  int cur = 0;
-  for (int ks0 = 0; ks0 < nks; ks0 += NST) {
-#pragma unroll
-    for (int u = 0; u < NST; ++u) {
-      const int ks = ks0 + u;
-      if (ks + NST - 1 < nks) issue(ks + NST - 1, (u + NST - 1) % NST, rb[(u + NST - 1) % NST]);
-#pragma unroll
-      for (int g = 0; g < KG; ++g) {
-        const int nxt = cur ^ 1;
-        if (g + 1 < KG) {
-          readA(u, g + 1, fa[nxt]);
-        } else if (ks + 1 < nks) {
-          // stage ks + 1 (its A in LDS, its B in registers) must have landed and every wave must
-          // be done reading stage ks's A before anyone refills it
-          const int later = (nks - 2 - ks) < (NST - 2) ? (nks - 2 - ks) : (NST - 2);
-          p3d_wait_stages<PER, NST>(later);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          __builtin_amdgcn_sched_barrier(0);
-          readA((u + 1) % NST, 0, fa[nxt]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = 0; c < CT; ++c)
-            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][r], rb[u][g][c], acc[r][c], 0, 0, 0);
-        cur = nxt;
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  // ---- epilogue (as k_gemm_bf16p) ----
-  float* et = (float*)smem;
-  const int i = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        et[(64 * wm + 16 * r + 4 * q + e) * 132 + 16 * CT * wn + 16 * c + i] = acc[r][c][e];
-  __syncthreads();
-  const int ngY = p.N / 32;
-#pragma unroll
-  for (int it = 0; it < 2048 / (64 * WAVES); ++it) {
-    const int item = it * 64 * WAVES + tid;
-    const int chunk = item >> 6, l = item & 63;
-    const int rl = 16 * (chunk >> 2) + (l & 15);
-    const int cl = 32 * (chunk & 3) + 8 * (l >> 4);
-    const int row = 128 * mt + rl, col = 128 * nt + cl;
-    const int64_t off = p3d_pk16(row, col, ngY);
-    u16x8 rv;
-    if (p.res) rv = *(const u16x8*)(p.res + off);
-    u16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int n = col + e;
-      float z = et[rl * 132 + cl + e] + p.epi.bias[n];
-      float y = p.epi.inv ? z * p.epi.inv[n] + p.epi.shift[n] : z;
-      if (p.epi.relu) y = fmaxf(y, 0.0f);
-      if (p.res) y += p3d_bf2f(rv[e]);
-      o[e] = p3d_f2bf(y);
-    }
-    *(u16x8*)(p.Y + off) = o;
-  }
-}
-
 // =====================================================================================
 // Split-K form for wide layers at modest M (cfg5: M = 1024, N = K = 4096).
 //

@@ -630,26 +630,6 @@ def test_bf16_inference_matches_emulated_oracle(L, N, B):
     m.close()
 
 
-@pytest.mark.skipif(os.environ.get("P3D_TEST_BF16R") != "1",
-                    reason="opt-in kernel (P3D_BF16_STAGES=99) not yet validated on the box")
-@pytest.mark.parametrize("L,N,B", [(4096, 4, 1024), (512, 1, 200), (256, 2, 128)])
-def test_bf16_register_b_bit_identical(L, N, B, monkeypatch):
-    """k_gemm_bf16r (A on the LDS-DMA ring, B loaded straight into registers, p3d_bf16.h) ==
-    k_gemm_bf16p (both operands through LDS), bit for bit: the same MFMAs in the same order."""
-    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
-    st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
-    x = torch.from_numpy(np.random.default_rng(B + 7).standard_normal((B, 32)).astype(np.float32)).cuda()
-    ys = []
-    for stages in ("99", "48"):
-        monkeypatch.setenv("P3D_BF16_STAGES", stages)
-        m = linear_model.LinearModel(L, N, True, True, False, B, 1e-3, "/tmp/p3d_test", dtype="bfloat16",
-                                     seed=3, max_batch=B)
-        m.set_weights({**st.params, **st.moving})
-        ys.append(m.forward_device(x).cpu())
-        m.close()
-    assert torch.equal(ys[0], ys[1])
-
-
 @pytest.mark.parametrize("max_norm,p14,B", [(False, False, 64), (True, False, 64), (False, True, 37), (False, False, 200)])
 def test_wgrad_multi_bit_identical(max_norm, p14, B, monkeypatch):
     """All layers' weight gradients in one k_wgrad_multi launch (default) == one k_wgrad
