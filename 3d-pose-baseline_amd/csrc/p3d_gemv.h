@@ -407,6 +407,25 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     p3d_pin<GC>(wf[t]);
     p3d_pin_epi(e[t]);
   }
+  // unNormalizeData's operands depend on no input: waves 1.. write the unused dimensions
+  // ((float) 0 * std + mean) and stage the used columns' index / std / mean in LDS while the
+  // producers finish, off the critical path behind the hand-off (registers: no room at 1024 threads)
+  __shared__ int od[64];
+  __shared__ double osd[64], omu[64];
+  if (f.fr.out && w != 0) {
+    for (int k = (int)threadIdx.x - 64; k < M * f.fr.D3; k += 64 * (WV - 1)) {
+      const int r = k / f.fr.D3, d = k - r * f.fr.D3;
+      bool used = false;
+      for (int u = 0; u < o.N; ++u) used |= f.fr.use3[u] == d;
+      if (!used) f.fr.out[(int64_t)r * f.fr.D3 + d] = p3d_unnorm_out(0.0f, f.fr.std3[d], f.fr.mean3[d]);
+    }
+    if (w == 1 && lane < o.N) {
+      const int d = f.fr.use3[lane];
+      od[lane] = d;
+      osd[lane] = f.fr.std3[d];
+      omu[lane] = f.fr.mean3[d];
+    }
+  }
   // ---- the hand-off: this launch's other workgroups' outputs ----------------------------------
   p3d_gemv_gather<64 * WV>(p3d_rsrc(f.hand), 0, M, K, tag, xs, f.err);
 #ifdef P3D_TRACE
@@ -434,15 +453,6 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     }
   }
   __syncthreads();
-  if (f.fr.out && w != 0) {
-    // unNormalizeData's unused dimensions: (float) 0 * std + mean (waves 1.., beside wave 0)
-    for (int k = (int)threadIdx.x - 64; k < M * f.fr.D3; k += 64 * (WV - 1)) {
-      const int r = k / f.fr.D3, d = k - r * f.fr.D3;
-      bool used = false;
-      for (int u = 0; u < o.N; ++u) used |= f.fr.use3[u] == d;
-      if (!used) f.fr.out[(int64_t)r * f.fr.D3 + d] = p3d_unnorm_out(0.0f, f.fr.std3[d], f.fr.mean3[d]);
-    }
-  }
   if (w != 0 || q >= M || q >= MR) return;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -454,10 +464,7 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     const float y = p3d_gemv_epi(o, e[t], zs, q, col < o.N ? col : o.N - 1);
     if (col < o.N) {
       if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
-      if (f.fr.out) {
-        const int d = f.fr.use3[col];
-        f.fr.out[(int64_t)q * f.fr.D3 + d] = p3d_unnorm_out(y, f.fr.std3[d], f.fr.mean3[d]);
-      }
+      if (f.fr.out) f.fr.out[(int64_t)q * f.fr.D3 + od[col]] = p3d_unnorm_out(y, osd[col], omu[col]);
     }
   }
 }

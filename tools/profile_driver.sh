@@ -6,6 +6,8 @@
 #      per launch (tools/pmc_traffic.py turns them into HBM bytes per launch)
 #   3. the same for the cfg3 training step (bench.py --mode train)
 #   4. kernel stats of the 1-rank data-parallel step (bench.py --dp1-child)
+#   5. MFMA busy of the cfg5 bf16 stress step (SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE, one pass
+#      each; tools/pmc_mfma.py turns them into matrix-pipe utilisation per kernel)
 # Every step under its own time limit; the script stops at the first failure.
 set -e
 OUT=${1:-gpurun_out/prof}
@@ -23,4 +25,8 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/trai
 # 4. the data-parallel step's form on a 1-rank RCCL group (what every rank runs at N > 1)
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dp1_trace" -o run -- \
     python3 bench.py --dp1-child --train-steps 400 > "$OUT/dp1_under_rocprof.json" 2> "$OUT/dp1_under_rocprof.err"
+# 5. matrix-pipe utilisation of the cfg5 bf16 stress step
+STRESS="python3 bench.py --gpus 1 --mode stress --steps 16 --warmup 4 --no-cpu"
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d "$OUT/stress_mfma" -o run -- $STRESS > "$OUT/stress_mfma.json" 2> "$OUT/stress_mfma.err"
+timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stress_grbm" -o run -- $STRESS > "$OUT/stress_grbm.json" 2> "$OUT/stress_grbm.err"
 echo profile-done
