@@ -340,32 +340,33 @@ __device__ __forceinline__ void p3d_gemv_fold_in(const GemvArgs& in, int own, fl
   __syncthreads();
 }
 
-// Every thread of the workgroup: rows r < M of a K-wide layer output handed over as granules
-// (granule j of row r = features 2j, 2j + 1, at rh + 16 (gbase + r K / 2 + j)) into xs[r][k], each
-// once its tag matches; then a barrier.
-template <int NT>
-__device__ __forceinline__ void p3d_gemv_gather(__amdgpu_buffer_rsrc_t rh, int gbase, int M, int K, unsigned tag,
-                                                float* xs, int* err) {
-  const int ng = M * (K >> 1);
-  for (int base = 0; base < ng; base += NT) {
-    const int j = base + (int)threadIdx.x;
-    if (j < ng) {
-      u32x4_t v;
-      for (int spin = 0;; ++spin) {
-        v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rh, (gbase + j) * 16, 0, 16));   // sc1
-        if (v.y == tag && v.w == tag) break;
-        if (spin > P3D_XCHG_SPIN) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+// One wave: rows r < M, features [16 gb, 16 ge) of a K-wide layer output handed over as granules
+// (granule j of row r = features 2j, 2j + 1, at rh + 16 (gbase + r K / 2 + j)) into the wave's own
+// columns of xs, each once its tag matches.  No workgroup
+// barrier: only this wave reads those columns (k_gemv's K split), so it contracts as soon as its
+// own producers have published, whatever the other waves still wait for.
+__device__ __forceinline__ void p3d_gemv_gather_wave(__amdgpu_buffer_rsrc_t rh, int gbase, int M, int K, int gb,
+                                                     int ge, unsigned tag, float* xs, int* err) {
+  const int lane = threadIdx.x & 63, per = 8 * (ge - gb);   // granules per row in the slice
+  for (int idx = lane; idx < M * per; idx += 64) {
+    const int r = idx / per, j = r * (K >> 1) + 8 * gb + (idx - r * per);
+    u32x4_t v;
+    for (int spin = 0;; ++spin) {
+      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rh, (gbase + j) * 16, 0, 16));   // sc1
+      if (v.y == tag && v.w == tag) break;
+      if (spin > P3D_XCHG_SPIN) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
       }
-      const int r = j / (K >> 1), k = 2 * (j - r * (K >> 1));
-      xs[r * K + k] = __uint_as_float(v.x);
-      xs[r * K + k + 1] = __uint_as_float(v.z);
+      __builtin_amdgcn_s_sleep(1);
     }
+    const int k = 2 * (j - r * (K >> 1));
+    xs[r * K + k] = __uint_as_float(v.x);
+    xs[r * K + k + 1] = __uint_as_float(v.z);
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Wave 0 of a tile's workgroup, all 64 lanes: lane (i even, q < M) stores columns col, col + 1 of
@@ -427,13 +428,10 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     }
   }
   // ---- the hand-off: this launch's other workgroups' outputs ----------------------------------
-  p3d_gemv_gather<64 * WV>(p3d_rsrc(f.hand), 0, M, K, tag, xs, f.err);
+  p3d_gemv_gather_wave(p3d_rsrc(f.hand), 0, M, K, gb, ge, tag, xs, f.err);
 #ifdef P3D_TRACE
   if (threadIdx.x == 0 && blockIdx.x == 0) g_p3d_trace[4] = wall_clock64();
 #endif
-  // every workgroup of the launch has read the epoch (each producer tagged with it): the slot's
-  // next launch gets a new tag
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (t >= nto) break;
@@ -453,6 +451,9 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     }
   }
   __syncthreads();
+  // every wave has seen its producers' granules, so every workgroup of the launch has read the
+  // epoch (each producer tagged with it): the slot's next launch gets a new tag
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (w != 0 || q >= M || q >= MR) return;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
     rv = __uint_as_float((i & 1) ? v.z : v.x);
   }
   // ---- this layer's input: layer l - 1's hand-off (slot 0: the input layer) --------------------
-  p3d_gemv_gather<64 * WV>(rh, (l - 1) * gpl, M, K, tag, xs, c.err);
+  p3d_gemv_gather_wave(rh, (l - 1) * gpl, M, K, gb, ge, tag, xs, c.err);
   P3D_CH_STAMP(1);
   // ---- contraction, quarters, waves (k_gemv) -------------------------------------------------
   float acc[MR];
