@@ -381,32 +381,38 @@ __device__ __forceinline__ void p3d_gemv_publish(__amdgpu_buffer_rsrc_t rh, int 
   }
 }
 
-// The output layer, by one workgroup: its weights first, then the hand-off of the M x K inputs
-// (this launch's other workgroups' outputs) into xs, then every 16-column tile as k_gemv<MR, WV, GC>
-// computes it (the same K split over the WV waves, the same chains and sums).
-template <int MR, int WV, int GC>
+// The output layer's column tiles [t0, t0 + NTO) (at most four: N <= 64), by one workgroup: their
+// weights first, then the hand-off of the M x K inputs (this launch's other workgroups' outputs)
+// into xs, then every tile as k_gemv<MR, WV, GC> computes it (the same K split over the WV waves,
+// the same chains and sums).  Which workgroup runs a tile does not change its bits: k_gemv_fold
+// gives all of them to one, k_gemv_chain one tile each to three (a workgroup's wave 0 contracting,
+// reducing and storing three tiles was 3 us of issue behind the last hand-off; one is 1).  The
+// workgroup with t0 = 0 advances the epoch and writes unNormalizeData's unused dimensions.
+template <int MR, int WV, int GC, int NTO>
 __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned tag, float* xs,
-                                                  float (*red)[WV][MR][16]) {
+                                                  float (*red)[WV][MR][16], int t0) {
   const GemvArgs& o = f.out;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
   const int M = o.M, K = o.K, ngK = K >> 4, nto = (o.N + 15) >> 4;   // nto <= 4
   const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
-  GemvEpi e[4];
-  f32x4 wf[4][GC];
+  const int t1 = t0 + NTO < nto ? t0 + NTO : nto;
+  GemvEpi e[NTO];
+  f32x4 wf[NTO][GC];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= nto) break;
+  for (int u = 0; u < NTO; ++u) {
+    const int t = t0 + u;
+    if (t >= t1) break;
     const int col = 16 * t + i, cc = col < o.N ? col : o.N - 1;
-    e[t].ctr = o.ctr;
-    if (w == 0 && q < M) p3d_gemv_epi_load(o, q, cc, e[t]);
-    p3d_gemv_preload<GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, wf[t]);
+    e[u].ctr = o.ctr;
+    if (w == 0 && q < M) p3d_gemv_epi_load(o, q, cc, e[u]);
+    p3d_gemv_preload<GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, wf[u]);
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= nto) break;
-    p3d_pin<GC>(wf[t]);
-    p3d_pin_epi(e[t]);
+  for (int u = 0; u < NTO; ++u) {
+    if (t0 + u >= t1) break;
+    p3d_pin<GC>(wf[u]);
+    p3d_pin_epi(e[u]);
   }
   // unNormalizeData's operands depend on no input: waves 1.. write the unused dimensions
   // ((float) 0 * std + mean) and stage the used columns' index / std / mean in LDS while the
@@ -414,11 +420,13 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
   __shared__ int od[64];
   __shared__ double osd[64], omu[64];
   if (f.fr.out && w != 0) {
-    for (int k = (int)threadIdx.x - 64; k < M * f.fr.D3; k += 64 * (WV - 1)) {
-      const int r = k / f.fr.D3, d = k - r * f.fr.D3;
-      bool used = false;
-      for (int u = 0; u < o.N; ++u) used |= f.fr.use3[u] == d;
-      if (!used) f.fr.out[(int64_t)r * f.fr.D3 + d] = p3d_unnorm_out(0.0f, f.fr.std3[d], f.fr.mean3[d]);
+    if (t0 == 0) {
+      for (int k = (int)threadIdx.x - 64; k < M * f.fr.D3; k += 64 * (WV - 1)) {
+        const int r = k / f.fr.D3, d = k - r * f.fr.D3;
+        bool used = false;
+        for (int u = 0; u < o.N; ++u) used |= f.fr.use3[u] == d;
+        if (!used) f.fr.out[(int64_t)r * f.fr.D3 + d] = p3d_unnorm_out(0.0f, f.fr.std3[d], f.fr.mean3[d]);
+      }
     }
     if (w == 1 && lane < o.N) {
       const int d = f.fr.use3[lane];
@@ -433,12 +441,13 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
   if (threadIdx.x == 0 && blockIdx.x == 0) g_p3d_trace[4] = wall_clock64();
 #endif
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= nto) break;
+  for (int u = 0; u < NTO; ++u) {
+    const int t = t0 + u;
+    if (t >= t1) break;
     float acc[MR];
 #pragma unroll
     for (int r = 0; r < MR; ++r) acc[r] = 0.f;
-    p3d_gemv_chain<MR, GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, M, wf[t],
+    p3d_gemv_chain<MR, GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, M, wf[u],
                            [&](int g, int r) { return *(const f32x4*)&xs[r * K + 16 * g + 4 * q]; }, acc);
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
@@ -447,22 +456,29 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     }
     if (q == 0) {
 #pragma unroll
-      for (int r = 0; r < MR; ++r) red[t][w][r][i] = acc[r];
+      for (int r = 0; r < MR; ++r) red[u][w][r][i] = acc[r];
     }
   }
+#ifdef P3D_TRACE
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_p3d_trace[6] = wall_clock64();
+#endif
   __syncthreads();
+#ifdef P3D_TRACE
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_p3d_trace[7] = wall_clock64();
+#endif
   // every wave has seen its producers' granules, so every workgroup of the launch has read the
   // epoch (each producer tagged with it): the slot's next launch gets a new tag
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0 && t0 == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (w != 0 || q >= M || q >= MR) return;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= nto) break;
+  for (int u = 0; u < NTO; ++u) {
+    const int t = t0 + u;
+    if (t >= t1) break;
     const int col = 16 * t + i;
     float zs = 0.f;
 #pragma unroll
-    for (int u = 0; u < WV; ++u) zs += red[t][u][q][i];
-    const float y = p3d_gemv_epi(o, e[t], zs, q, col < o.N ? col : o.N - 1);
+    for (int v = 0; v < WV; ++v) zs += red[u][v][q][i];
+    const float y = p3d_gemv_epi(o, e[u], zs, q, col < o.N ? col : o.N - 1);
     if (col < o.N) {
       if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
       if (f.fr.out) f.fr.out[(int64_t)q * f.fr.D3 + od[col]] = p3d_unnorm_out(y, osd[col], omu[col]);
@@ -481,7 +497,7 @@ __global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
   const int i = lane & 15, q = lane >> 4;
   const unsigned tag = f.fout ? __hip_atomic_load(f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
   if (f.fout && blockIdx.x == gridDim.x - 1) {
-    p3d_gemv_fold_out<MR, WV, GC>(f, tag, xs, red);
+    p3d_gemv_fold_out<MR, WV, GC, 4>(f, tag, xs, red, 0);
     return;
   }
   const int ct = blockIdx.x;
@@ -543,10 +559,11 @@ __global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
 // (K = 32) is computed by layer 2's workgroups, tile t each, as their first act (hand-off slot 0):
 // recomputing all of it in every layer-1 workgroup (k_gemv_fold's way) meant 128 KB of input-layer
 // weights per CU, the longest phase of the launch (tools/trace_chain.py).  Its tile is layer 2's
-// residual too; later blocks read theirs from layer l - 2's hand-off.  Workgroup 0 (layer 1, tile
-// 0; idle once its tile is out) then runs the output layer on the last layer's hand-off
-// (p3d_gemv_fold_out) and advances the slot's epoch: every workgroup has read the epoch by then
-// (each published with its tag, and each layer's tiles were all gathered by the next layer's).
+// residual too; later blocks read theirs from layer l - 2's hand-off.  Workgroups 0 .. 2 (layer 1,
+// tiles 0 .. 2; idle once their tiles are out) then run an output-layer tile each on the last
+// layer's hand-off (p3d_gemv_fold_out), and workgroup 0 advances the slot's epoch: every workgroup
+// has read the epoch by then (each published with its tag, and each layer's tiles were all
+// gathered by the next layer's).
 // Every wait is bounded (err); the launch needs its grid resident (host: H L / 16 <= CUs).  Same
 // k_gemv arithmetic throughout, so the same bits as the six launches
 // (tests/test_gpu_parity.py::test_gemv_small_batch).
@@ -576,7 +593,8 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
 #ifdef P3D_TRACE   // development builds (tools/trace_chain.py): per workgroup at 8 b: start, input,
-                   // contracted, published; workgroup 0 also output gathered (4), end (5)
+                   // contracted, published; workgroup 0 also output gathered (4), end (5),
+                   // its output tile contracted (6) and reduced (7)
 #define P3D_CH_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 512) g_p3d_trace[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
 #else
 #define P3D_CH_STAMP(k) do { } while (0)
@@ -664,8 +682,8 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
 #endif
     P3D_CH_STAMP(3);
   }
-  if (b != 0) return;
-  // ---- workgroup 0: the output layer on the last layer's hand-off -------------------------------
+  if (b >= ((c.out.N + 15) >> 4)) return;
+  // ---- workgroups 0 .. N_out / 16 - 1: an output-layer tile each, on the last layer's hand-off ----
   GemvFold f{};
   f.fout = 1;
   f.out = c.out;
@@ -673,6 +691,6 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   f.epoch = c.epoch;
   f.err = c.err;
   f.fr = c.fr;
-  p3d_gemv_fold_out<MR, WV, 4>(f, tag, xs, red);
+  p3d_gemv_fold_out<MR, WV, 4, 1>(f, tag, xs, red, b);
   P3D_CH_STAMP(5);
 }

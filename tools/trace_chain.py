@@ -6,7 +6,7 @@
 
 Per hidden layer: median / max over its workgroups of start, input ready (input layer computed
 or the previous layer gathered), contracted, published; then workgroup 0's output-layer gather and
-end.  Times in us from the earliest workgroup start (wall_clock64, 100 MHz)."""
+end (wave 0's gather, its contraction, the reduction barrier, the epilogue's end).  Times in us from the earliest workgroup start (wall_clock64, 100 MHz)."""
 import ctypes
 import json
 import os
@@ -43,7 +43,8 @@ def main():
             blk = us[64 * l:64 * (l + 1)]
             layers["layer%d" % (l + 1)] = {name: [round(float(np.median(blk[:, k])), 2), round(float(blk[:, k].max()), 2)]
                                            for k, name in enumerate(("start", "input", "contracted", "published"))}
-        layers["out"] = {"gathered": round(float(us[0, 4]), 2), "end": round(float(us[0, 5]), 2)}
+        layers["out"] = {"gathered": round(float(us[0, 4]), 2), "contracted": round(float(us[0, 6]), 2),
+                         "barrier": round(float(us[0, 7]), 2), "end": round(float(us[0, 5]), 2)}
         out.append(layers)
         print(json.dumps({"rep": rep, **layers}), flush=True)
 
