@@ -611,6 +611,9 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   const int M = p.M, K = p.K, N = p.N, ngK = K >> 4;
   const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
   const int col = 16 * t + i;
+#ifdef P3D_TRACE
+  if (b >= 3) P3D_CH_STAMP(5);   // the layer's arguments in hand
+#endif
   const __amdgpu_buffer_rsrc_t rh = p3d_rsrc(c.hand);
   const int gpl = 4 * (N >> 1);                  // granules per layer
   // ---- the weight slice, then the epilogue operands (wave 0, lane (i, q) = row q, column col) ---
@@ -630,6 +633,10 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
     }
     p3d_gemv_publish(rh, 0, M, N, col, v0, tag);
     rv = v0;
+#ifdef P3D_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    P3D_CH_STAMP(4);   // the input layer's tile published
+#endif
   }
   const f32x4* pw = (const f32x4*)p.Wf + (int64_t)t * ngK * 64 + lane;
   f32x4 wf[GC];

@@ -43,6 +43,8 @@ def main():
             blk = us[64 * l:64 * (l + 1)]
             layers["layer%d" % (l + 1)] = {name: [round(float(np.median(blk[:, k])), 2), round(float(blk[:, k].max()), 2)]
                                            for k, name in enumerate(("start", "input", "contracted", "published"))}
+        layers["layer2"]["in_published"] = [round(float(np.median(us[64:128, 4])), 2), round(float(us[64:128, 4].max()), 2)]
+        layers["args_ready"] = [round(float(np.median(us[3:256, 5])), 2), round(float(us[3:256, 5].max()), 2)]
         layers["out"] = {"gathered": round(float(us[0, 4]), 2), "contracted": round(float(us[0, 6]), 2),
                          "barrier": round(float(us[0, 7]), 2), "end": round(float(us[0, 5]), 2)}
         out.append(layers)
