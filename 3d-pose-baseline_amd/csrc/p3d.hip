@@ -1756,6 +1756,9 @@ struct p3d_model {
   int dp_adam = 1;               // env P3D_DP_ADAM: 1 per-bucket optimizer on the compute stream behind its
                                  // all-reduce, 0 one optimizer pass after the last bucket, 2 per bucket on the
                                  // comm stream (round 3's form: slows the neighbouring dgrad launches)
+  int dp_force_multi = 0;        // env P3D_DP_FORCE_MULTI=1 (tests, bench): a 1-rank group takes the N > 1 form
+                                 // -- comm-stream fork, per-bucket ncclAvg, rev joins -- so the single-GPU box
+                                 // executes and times the code every rank of an 8-GPU run executes
   int serve_w4 = 5;         // k_serve variant (env P3D_SERVE_W4): 5 = k_serve5 (4-wave workgroups, pipelined
                             // steps), 0 = k_serve (8-wave, measured slower); num_layers = 0 always runs k_serve
   // live kernel timing (p3d_profile_start/stop): one hipEvent pair per launch
@@ -2082,11 +2085,15 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
       const int64_t nh = (int64_t)m->gemv_slots * m->gemv_slot_floats;
       if ((e = hipMalloc(&m->gemv_hand, nh * sizeof(float))) != hipSuccess) return cleanup(e);
       if ((e = hipMemset(m->gemv_hand, 0, nh * sizeof(float))) != hipSuccess) return cleanup(e);
-      if ((e = hipMalloc(&m->lift_x, (size_t)c.max_batch * c.input_size * sizeof(float))) != hipSuccess) return cleanup(e);
-      if ((e = hipMalloc(&m->lift_y, (size_t)c.max_batch * c.output_size * sizeof(float))) != hipSuccess) return cleanup(e);
       const int64_t ne = (int64_t)m->gemv_slots * P3D_XCHG_EPOCH_STRIDE;
       if ((e = hipMalloc(&m->gemv_epoch, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
       if ((e = hipMemset(m->gemv_epoch, 0, ne * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+    }
+    if (c.dtype == P3D_DTYPE_F32) {
+      // p3d_lift's three-step form (any batch; every float32 model, whether or not the batch <= 4
+      // fold / chain is configured): normalised rows and network outputs
+      if ((e = hipMalloc(&m->lift_x, (size_t)c.max_batch * c.input_size * sizeof(float))) != hipSuccess) return cleanup(e);
+      if ((e = hipMalloc(&m->lift_y, (size_t)c.max_batch * c.output_size * sizeof(float))) != hipSuccess) return cleanup(e);
     }
     if ((e = hipHostMalloc((void**)&m->errw, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
       return cleanup(e);
@@ -2098,6 +2105,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   }
   if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
   if (const char* ev = getenv("P3D_DP_ADAM")) m->dp_adam = atoi(ev);
+  if (const char* ev = getenv("P3D_DP_FORCE_MULTI")) m->dp_force_multi = atoi(ev) != 0;
   if (const char* ev = getenv("P3D_W_MASTER")) m->w_pk = atoi(ev) ? 0 : 1;
   if (m->cfg.max_norm) m->w_pk = 0;   // (||W||^2 of the max-norm scale is summed over the master)
   if (const char* ev = getenv("P3D_XCHG_REMAP")) m->xchg_remap = atoi(ev);
@@ -3761,6 +3769,10 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
     }
   } else if (what == 1) {
     n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
+  } else if (what == 6) {
+    // the optimizers' weight source (bench.py's byte count): "packed" = W read from its Wd copy, the
+    // TF-layout master not written (28 B per weight element per fused step); "master" = 32 B
+    n = m->w_pk ? "packed" : "master";
   } else if (what == 3 && !m->serve_kname.empty()) {
     n = m->serve_kname;     // the kernel the last p3d_serve launched
   } else if (what == 3) {
@@ -3962,7 +3974,7 @@ extern "C" int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, 
   if (B <= 0 || B > c.max_batch) return fail(P3D_ERR_ARG, "p3d_lift: batch must be in 1..max_batch");
   if (U2 != c.input_size || U3 != c.output_size || D2 < U2 || D3 < U3 || D3 > 256)
     return fail(P3D_ERR_ARG, "p3d_lift: dimension sets do not match the model");
-  if (c.dtype != P3D_DTYPE_F32 || !m->lift_x) return fail(P3D_ERR_ARG, "p3d_lift: float32 models with the batch<=4 path");
+  if (c.dtype != P3D_DTYPE_F32 || !m->lift_x) return fail(P3D_ERR_ARG, "p3d_lift: float32 models only");
   hipStream_t st = (hipStream_t)stream;
   if (B <= m->gemv_maxb) {
     GemvFrames fr{};

@@ -70,9 +70,13 @@ void bucket_range(const p3d_model* m, int k, int64_t& fb, int64_t& fe) {
   fe = hi + 1 < nl ? m->layers[hi + 1].w : m->n_flat;
 }
 
+// the N > 1 form: several ranks, or one forced into it (P3D_DP_FORCE_MULTI)
+bool dp_multi(const p3d_model* m) { return m->comm->nranks > 1 || m->dp_force_multi; }
+
 int dp_allreduce(p3d_model* m, float* buf, int64_t n, hipStream_t st) {
-  // in place; the identity on one rank (nothing enqueued), the replica mean otherwise
-  const ncclRedOp_t op = m->comm->nranks == 1 ? ncclSum : ncclAvg;
+  // in place; the identity on one rank (nothing enqueued), the replica mean otherwise (ncclAvg: on a
+  // forced 1-rank group the mean of one replica, still the identity)
+  const ncclRedOp_t op = dp_multi(m) ? ncclAvg : ncclSum;
   const ncclResult_t r = g_rccl.all_reduce(buf, buf, (size_t)n, ncclFloat32, op, m->comm->nc, st);
   return r == ncclSuccess ? P3D_OK : rccl_fail("p3d_train_step_dp: ncclAllReduce", r);
 }
@@ -182,10 +186,10 @@ extern "C" int p3d_train_step_dp(p3d_model* m, const float* x, const float* t, i
   const bool bucketed = nb > 0 && !m->cfg.max_norm && m->wgrad_multi && (int)m->bucket_lo.size() == nb &&
                         (int)m->bat.size() == nb;
   if (!bucketed) {
-    if (m->comm->nranks > 1 && (rc = dp_allreduce(m, m->flat[1], m->n_flat, st))) return rc;
+    if (dp_multi(m) && (rc = dp_allreduce(m, m->flat[1], m->n_flat, st))) return rc;
     return p3d_adam_apply(m, stream);
   }
-  if (m->comm->nranks == 1) {
+  if (!dp_multi(m)) {
     // one replica: the mean of the gradients is the gradient itself and RCCL enqueues nothing for
     // it, so no comm-stream branch either (a forked branch in a captured graph puts its edges on
     // another hardware queue and slowed every launch of the step by 0.4-0.7 us, r04 A/B): each

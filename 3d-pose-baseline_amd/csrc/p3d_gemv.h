@@ -98,7 +98,7 @@ __device__ __forceinline__ void p3d_gemv_chain(const f32x4* pw, int gb, int ge, 
     if (g0 != gb) {
 #pragma unroll
       for (int j = 0; j < GC; ++j) {
-        const int g = g0 + j < ge ? g0 + j : ge - 1;
+        const int g = g0 + j < ge ? g0 + j : ge - 1;   // (here ge > g0 >= gb: in the slice)
         wf[j] = pw[(int64_t)g * 64];
       }
     }
@@ -131,11 +131,16 @@ __device__ __forceinline__ void p3d_pin(f32x4 (&v)[GC]) {
 __device__ __forceinline__ void p3d_pin_epi(GemvEpi& e) {
   asm volatile("" : "+v"(e.b), "+v"(e.gam), "+v"(e.bet), "+v"(e.mmu), "+v"(e.mva), "+v"(e.rv), "+v"(e.mxv));
 }
+// (Loads past the slice's end re-read its last fragment, unused.  A wave's slice is EMPTY when the
+// layer has fewer K groups than the workgroup has waves (K < 16 WV, e.g. L < 256 at 16 waves): gb ==
+// ge, and the clamp must not step to ge - 1 = gb - 1 -- for wave 0 of tile 0 that is the 1 KB in
+// front of the weight buffer, a read outside the allocation.  Clamped to gb, which is < ngK.)
 template <int GC>
 __device__ __forceinline__ void p3d_gemv_preload(const f32x4* pw, int gb, int ge, f32x4 (&wf)[GC]) {
+  const int glast = ge > gb ? ge - 1 : gb;
 #pragma unroll
   for (int j = 0; j < GC; ++j) {
-    const int g = gb + j < ge ? gb + j : ge - 1;
+    const int g = gb + j < ge ? gb + j : glast;
     wf[j] = pw[(int64_t)g * 64];   // default policy: frame after frame hits the XCD's L2 / MALL
   }
 }

@@ -120,6 +120,21 @@ def allreduce_sum_(t):
 
 
 _NATIVE = {}
+_ATTACHED = None   # weakref.WeakSet of the models attached to a cached communicator
+
+
+def attach_native(model):
+    """Attach ``model`` to the process's library-owned communicator (p3d_dp_attach) and remember
+    it, so that close_native_comms can detach it before the communicator is destroyed."""
+    import weakref
+    import _p3d
+    global _ATTACHED
+    if _ATTACHED is None:
+        _ATTACHED = weakref.WeakSet()
+    h = native_comm()
+    _p3d.check(_p3d.lib().p3d_dp_attach(model._h, h), "p3d_dp_attach")
+    _ATTACHED.add(model)
+    return h
 
 
 def librccl_path():
@@ -169,6 +184,15 @@ def close_native_comms():
     if not _NATIVE:
         return
     torch.cuda.synchronize()
+    # models first: a model still holding the communicator would reduce over a freed ncclComm
+    for model in list(_ATTACHED or ()):
+        h = getattr(model, "_h", None)
+        if h is not None and h.value:
+            _p3d.check(_p3d.lib().p3d_dp_attach(h, None), "p3d_dp_attach")
+        model._native = None
+        model._buckets = False      # the next DP step re-plans (and re-attaches)
+    if _ATTACHED is not None:
+        _ATTACHED.clear()
     for k in list(_NATIVE):
         _p3d.check(_p3d.lib().p3d_comm_destroy(_NATIVE.pop(k)), "p3d_comm_destroy")
 

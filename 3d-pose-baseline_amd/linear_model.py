@@ -304,11 +304,16 @@ class LinearModel(object):
             return (L, L)
         return (numel,)
 
-    def variable(self, name):
-        """Zero-copy torch view (device) of a TF-named variable."""
+    def variable(self, name, sync=True):
+        """Zero-copy torch view (device) of a TF-named variable.  ``sync=False`` takes the view
+        without bringing the weight masters up to date first (the caller already did: a re-derive
+        between two host writes would overwrite the first with the packed copy)."""
         for n, numel, kind, off in self.param_table:
             if n == name:
-                buf = self.flat["params"] if kind == 0 else self.flat["moving"]
+                if kind == 0:
+                    buf = self.flat["params"] if sync else dict.__getitem__(self.flat, "params")
+                else:
+                    buf = self.flat["moving"]
                 return buf[off:off + numel].view(self._shapes[name])
         raise KeyError(name)
 
@@ -373,23 +378,25 @@ class LinearModel(object):
         torch = self.torch
         self.sync_params()   # a subset: the other masters must be current before the re-pack
         for name, val in arrays.items():
-            v = self.variable(name)
+            v = self.variable(name, sync=False)   # ONE sync: after a captured optimizer every
+            # sync re-derives the masters from Wd, which would undo the writes before this one
             a = np.asarray(val, dtype=np.float32).reshape(v.shape)
             v.copy_(torch.from_numpy(np.ascontiguousarray(a)))
         self.params_updated()
 
     def get_weights(self, include_moving=True):
         out = {}
+        self.sync_params()
         for name, numel, kind, off in self.param_table:
             if kind == 0 or include_moving:
-                out[name] = self.variable(name).detach().cpu().numpy().copy()
+                out[name] = self.variable(name, sync=False).detach().cpu().numpy().copy()
         return out
 
     def get_state(self):
         """Every global variable (tf.global_variables()) as numpy, TF names."""
         st = self.get_weights(include_moving=True)
         for name in self.trainable_names():
-            numel = self.variable(name).numel()
+            numel = int(np.prod(self._shapes[name]))
             off = [o for n, _, k, o in self.param_table if n == name][0]
             st[name + "/Adam"] = self.flat["adam_m"][off:off + numel].cpu().numpy().reshape(self._shapes[name])
             st[name + "/Adam_1"] = self.flat["adam_v"][off:off + numel].cpu().numpy().reshape(self._shapes[name])
@@ -405,7 +412,7 @@ class LinearModel(object):
         self.set_weights({k: v for k, v in st.items() if k in self._shapes})
         for name in self.trainable_names():
             off = [o for n, _, k, o in self.param_table if n == name][0]
-            numel = self.variable(name).numel()
+            numel = int(np.prod(self._shapes[name]))
             if name + "/Adam" in st:
                 self.flat["adam_m"][off:off + numel].copy_(torch.from_numpy(
                     np.ascontiguousarray(st[name + "/Adam"], np.float32).reshape(-1)))
@@ -641,11 +648,12 @@ class LinearModel(object):
             if env is not None:
                 bucket_mb = float(env)
             else:
-                bucket_mb = 8.0 if dist.is_initialized() and dist.get_world_size() > 1 else 0.0
+                multi = (dist.is_initialized() and dist.get_world_size() > 1) or \
+                    os.environ.get("P3D_DP_FORCE_MULTI", "0") not in ("", "0")   # (the N > 1 form on 1 rank)
+                bucket_mb = 8.0 if multi else 0.0
         nccl = self.data_parallel and dist.is_initialized() and dist.get_backend() == "nccl"
         if nccl and getattr(self, "_native", None) is None:
-            self._native = dist_utils.native_comm()
-            check(lib().p3d_dp_attach(self._h, self._native), "p3d_dp_attach")
+            self._native = dist_utils.attach_native(self)
         # gloo path: each bucket's optimizer right behind its host all-reduce (p3d_adam_apply_bucket);
         # P3D_DP_BUCKET_ADAM=0: one p3d_adam_apply after the last bucket (RCCL: env P3D_DP_ADAM)
         self._bucket_adam = os.environ.get("P3D_DP_BUCKET_ADAM", "1") != "0"

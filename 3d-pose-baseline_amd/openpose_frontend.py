@@ -89,7 +89,13 @@ class FrameLifter:
 
     def _body(self):
         self.din.copy_(self.hin, non_blocking=True)
-        lift(self.model, self.din, self.m2, self.s2, self.u2, self.m3, self.s3, self.u3, out=self.p3)
+        if self.model.bf16:
+            # p3d_lift is float32-only: the three calls it folds (the same arithmetic)
+            dp.normalize(self.din, self.m2, self.s2, self.u2, out_dtype=self.torch.float32, out=self.x)
+            self.model.forward_device(self.x, False, 1.0, out=self.y, ctr=0)
+            dp.unnormalize(self.y, self.m3, self.s3, self.u3, self.p3.shape[1], out=self.p3)
+        else:
+            lift(self.model, self.din, self.m2, self.s2, self.u2, self.m3, self.s3, self.u3, out=self.p3)
         self.hout.copy_(self.p3, non_blocking=True)
 
     def lift_mapped(self, enc_in64):

@@ -480,7 +480,10 @@ def main(argv=None):
     FLAGS = build_parser().parse_args(argv)
     if FLAGS.sample:
         raise NotImplementedError("sample() is matplotlib visualisation (out of scope for this build)")
-    return train(FLAGS)
+    try:
+        return train(FLAGS)
+    finally:
+        dist_utils.close_native_comms()   # data parallel over RCCL: detach the model, free the comm
 
 
 if __name__ == "__main__":

@@ -297,7 +297,8 @@ int p3d_mpjpe_accum_ex(const float* pred_n, const float* gt_n, int32_t D, const 
  * 0 = inference hidden layer at B <= 64, 1 = inference hidden layer at large M,
  * 2 = BN-train hidden-layer GEMM, 3 = the kernel of the last p3d_serve launch,
  * 4 = inference hidden layer at B <= 4 (weight-streaming GEMV), 5 = the kernel of the last bf16
- * hidden layer (empty before one ran).  (Measurement plumbing for bench.py.) */
+ * hidden layer (empty before one ran), 6 = the optimizers' weight source: "packed" (W read from its
+ * packed Wd copy, the TF-layout master not written) or "master".  (Measurement plumbing for bench.py.) */
 int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int64_t out_len);
 
 /* Host-binding plumbing: a DLPack v0.8 DLManagedTensor aliasing `data` (no copy; the

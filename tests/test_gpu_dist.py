@@ -307,7 +307,9 @@ def _check_dp_free_running(r, L, steps, tag="bucketed"):
     worst = max(stats, key=lambda k: stats[k][0])
     print("free-running DP, %d steps: worst %s hip %.3g (float32 oracle %.3g)" % (steps, worst, *stats[worst]))
     for n, (hip, f32) in stats.items():
-        assert hip <= 2 * f32 + 1e-3, (n, hip, f32)
+        # a floor scaled to the measured drift (worst tensor 3.1e-5 vs the float32
+        # oracle's 3.8e-5), so a DP-path error of 1e-4 relative fails
+        assert hip <= 2 * f32 + 1e-5, (n, hip, f32)
     return stats
 
 
@@ -435,11 +437,17 @@ def _worker_rccl_graph(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_dp_rccl_step_graph_capture(tmp_path):
+@pytest.mark.parametrize("force_multi", ["0", "1"])
+def test_dp_rccl_step_graph_capture(tmp_path, monkeypatch, force_multi):
     """The RCCL data-parallel step captured in ONE HIP graph (the bucket all-reduces captured on
     the comm stream, forked from the step by the bucket events and joined before Adam): a 1-rank
     RCCL group (the box has one GPU), 2 buckets at cfg3's size; the captured step == the eager DP
-    step, and (average of one replica) == the fused single-GPU step, bit for bit."""
+    step, and (average of one replica) == the fused single-GPU step, bit for bit.
+    force_multi = 1 (P3D_DP_FORCE_MULTI): the 1-rank group takes p3d_train_step_dp's
+    N > 1 branch -- the comm-stream fork, one ncclAllReduce(ncclAvg) per bucket behind its
+    gradient-ready event, the rev joins, per-bucket Adam on the compute stream -- the code every
+    rank of an 8-GPU run executes, captured and eager, still bit-identical to the fused step."""
+    monkeypatch.setenv("P3D_DP_FORCE_MULTI", force_multi)
     out = str(tmp_path / "r.npz")
     mp.spawn(_worker_rccl_graph, args=(1, free_port(), out), nprocs=1, join=True)
     r = np.load(out)

@@ -93,3 +93,23 @@ def test_lift_bit_identical_to_three_steps(B, monkeypatch):
         outs.append(out.cpu())
         m.close()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("env", [("P3D_GEMV_FOLD", "0"), ("P3D_GEMV_MAXB", "0")])
+def test_frame_lifter_without_batch4_forms(env, monkeypatch):
+    """Advisor r4 (medium): FrameLifter must work where the batch <= 4 fold / chain is not
+    configured (p3d_lift then runs its three steps itself): without the fold the six k_gemv
+    launches give the chain's bits; without the batch <= 4 forms (P3D_GEMV_MAXB=0) the 16-row
+    MFMA kernels run (another summation order): the MLP tolerance."""
+    st, m, s, use2, use3, ign3, frames = setup()
+    ref = of.FrameLifter(m, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3, batch=1).lift(frames[:5])
+    m.close()
+    monkeypatch.setenv(*env)
+    st, m, s, use2, use3, ign3, frames = setup()
+    got = of.FrameLifter(m, s["mean2"], s["std2"], use2, s["mean3"], s["std3"], ign3, batch=1).lift(frames[:5])
+    if env[0] == "P3D_GEMV_FOLD":
+        np.testing.assert_array_equal(got, ref)
+    else:
+        assert np.abs(got - ref).max() <= 1e-4 * s["std3"].max()
+    m.check_errors()
+    m.close()

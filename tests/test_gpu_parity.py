@@ -105,7 +105,10 @@ def _gemv_tags(m, fn):
     (1024, 2, 1, True, True, False, 1.0, False), (1024, 2, 2, True, True, False, 1.0, False),
     (1024, 2, 3, True, True, True, 1.0, False), (1024, 2, 4, True, True, False, 0.5, False),
     (256, 3, 1, False, True, False, 1.0, False), (256, 1, 4, True, False, False, 1.0, True),
-    (2048, 1, 2, True, True, False, 1.0, False)])
+    (2048, 1, 2, True, True, False, 1.0, False),
+    # L < 256: fewer K groups than the 16 waves, empty wave slices (their clamped weight loads
+    # must stay inside the slice: round 5)
+    (64, 2, 1, True, True, False, 1.0, False), (128, 1, 3, True, True, False, 0.5, False)])
 def test_gemv_small_batch(L, N, B, residual, batch_norm, max_norm, keep, p14, monkeypatch):
     """Batch <= 4 inference through the weight-streaming k_gemv layers (the per-frame call of
     src/openpose_3dpose_sandbox.py:353-356) vs the fp64 oracle; rows independent (every row
@@ -751,3 +754,37 @@ def test_optimizer_from_packed_weights_bit_identical(monkeypatch, dp):
         m.close()
     for k, v in res["master"].items():
         np.testing.assert_array_equal(np.asarray(res["packed"][k]), np.asarray(v), err_msg=k)
+
+
+def test_set_weights_after_captured_step_keeps_every_write():
+    """Advisor r4 (high): after a captured optimizer replays, every parameter sync re-derives the
+    weight masters from Wd.  set_weights / set_state of SEVERAL weights must sync once, not per
+    weight (a re-derive between two writes would undo the first).  Replay a captured training step,
+    write every trainable, read them all back; then a restore of a saved state round-trips."""
+    m = linear_model.LinearModel(256, 2, True, True, False, 64, 1e-3, "/tmp/p3d_sw", seed=3, max_batch=64)
+    m.initialize(seed=9)
+    rng = np.random.default_rng(8)
+    xb = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+    tb = torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda()
+    step = m.train_step_graph(xb, tb, 0.5)
+    step()
+    step()
+    torch.cuda.synchronize()
+    saved = {k: np.array(v, copy=True) for k, v in m.get_state().items()}
+    new = {n: rng.standard_normal(m._shapes[n]).astype(np.float32) for n in m.trainable_names()}
+    m.set_weights(new)
+    got = m.get_weights(include_moving=False)
+    for n, v in new.items():
+        np.testing.assert_array_equal(got[n], v, err_msg=n)
+    # the packed copies follow: an eval forward equals a fresh model holding the same weights
+    x = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+    y1 = m.forward_device(x).cpu().numpy()
+    m2 = linear_model.LinearModel(256, 2, True, True, False, 64, 1e-3, "/tmp/p3d_sw2", seed=3, max_batch=64)
+    m2.set_state(dict(saved, **new))
+    np.testing.assert_array_equal(m2.forward_device(x).cpu().numpy(), y1)
+    m.set_state(saved)
+    st = m.get_state()
+    for k, v in saved.items():
+        np.testing.assert_array_equal(np.asarray(st[k]), np.asarray(v), err_msg=k)
+    m.close()
+    m2.close()

@@ -1,0 +1,75 @@
+"""Build-time guard: the hot kernels of the built libp3d.so use NO scratch.
+
+A private array indexed with a value the compiler cannot resolve to a constant after unrolling is
+placed in scratch memory (AMDGPU promotes an array to registers only when every index is constant),
+and so is a register spill.  Either way its private_segment_fixed_size becomes non-zero.  The
+persistent kernels sit at the register limit with runtime-bounded loops over private arrays
+(k_gemv_chain's wf / acc / e, k_serve6's rings); a runtime index that can leave its array is only
+possible once the array lives in scratch, and the round-4 chain build that spilled faulted on its
+first box run.  This test reads the gfx950 code object's metadata in the build
+container (tools/kernel_resources.py: no GPU), so a future spill fails here, not on the box.
+"""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "3d-pose-baseline_amd", "libp3d.so")
+
+# the kernels on the default paths (rocprof names); every one must be spill- and scratch-free
+HOT = [
+    "void k_gemv_chain<4, 4>(GemvChain)",            # batch <= 4 forward, one launch
+    "void k_serve6<4, 3, 2, 10>(ServeArgs)",          # the headline: 20 batch-64 requests per launch
+    "void k_serve6<4, 3, 2, 1>(ServeArgs)",           # one batch-64 request
+    "void k_serve6<4, 3, 2, 2>(ServeArgs)",
+    "void k_gemm_bf16p<64, 4, 8, false, 0, false>",   # cfg5 hidden layer
+    "k_wgrad_multi",                      # cfg3 weight gradients + fused TF1 Adam
+    "k_adam_pack",                                    # DP optimizer
+    "void k_fwd<1, 8, 8, 2, true, true, 1>(FwdArgs)",  # BN-train hidden forward (exchange form)
+    "void k_gemm_f32<2, 2, true>",                    # cfg4 large-M hidden layer
+    "void k_gemm_f32<2, 2, false>",                   # cfg4 large-M input layer
+]
+
+
+def _resources():
+    if not os.path.exists(LIB):
+        pytest.skip("libp3d.so not built")
+    if not all(os.path.exists(os.path.join("/opt/rocm/lib/llvm/bin", t))
+               for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf")):
+        pytest.skip("ROCm LLVM tools not present")
+    from tools.kernel_resources import kernel_resources
+    return kernel_resources(LIB)
+
+
+@pytest.fixture(scope="module")
+def res():
+    return _resources()
+
+
+def _find(res, name):
+    if name in res:
+        return res[name]
+    # match on the kernel and its template arguments (the argument list left out)
+    head = name.split("(")[0]
+    hits = [k for k in res if k.split("(")[0] == head]
+    assert hits, "kernel %s not in the code object (renamed? update HOT)" % name
+    return res[hits[0]]
+
+
+@pytest.mark.parametrize("name", HOT)
+def test_hot_kernel_uses_no_scratch(res, name):
+    r = _find(res, name)
+    assert r.get("private_segment_fixed_size", 0) == 0, (name, r)
+    # (SGPR spills go to VGPR lanes, v_writelane / v_readlane: no memory)
+    assert r.get("vgpr_spill_count", 0) == 0, (name, r)
+    assert not r.get("uses_dynamic_stack", False), (name, r)
+
+
+def test_no_kernel_uses_dynamic_stack(res):
+    """No kernel calls a function with a run-time stack (an un-inlined call: its stack size is a
+    runtime default, not something the metadata bounds)."""
+    bad = [k for k, r in res.items() if r.get("uses_dynamic_stack")]
+    assert not bad, bad
