@@ -25,6 +25,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ unsigned long long g_p3d_trace[4096 * 8];
 #endif
 
+// buffer resource over a whole allocation (raw buffer loads / stores with scalar offsets)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+// 16-B load with sc1 (bypasses this CU's L1; served by the XCD's L2): every read of data
+// another CU of the group produced goes through this
+__device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
+}
+
 // float offset of element (r, c) in a packed matrix with ng = C/16 column groups
 __device__ __host__ __forceinline__ int64_t p3d_pk(int r, int c, int ng) {
   return (((int64_t)(r >> 4) * ng + (c >> 4)) << 8) + (((r & 15) + ((c & 15) >> 2) * 16) << 2) + (c & 3);

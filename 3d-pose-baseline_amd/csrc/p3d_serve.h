@@ -122,14 +122,6 @@ struct ServeArgs {
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-// 16-B load with sc1 (bypasses this CU's L1; served by the XCD's L2): every read of data
-// another CU of the group produced goes through this
-__device__ __forceinline__ f32x4 p3d_ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
-}
 
 // Census (thread 0 of every workgroup): the XCD id read from the hardware, the workgroup's
 // rank within its XCD (one returning atomic on that XCD's counter), then a wait until the

@@ -45,7 +45,9 @@
 #pragma once
 #include "p3d_kernels.h"
 
+#ifndef P3D_XCHG_MAXR
 #define P3D_XCHG_MAXR 16          // row tiles per exchange (B <= 256)
+#endif
 #define P3D_XCHG_SPIN (1 << 19)
 
 // ---- arithmetic shared by the split and exchange forms (no FMA contraction) -------------
@@ -160,9 +162,10 @@ __device__ __forceinline__ void p3d_xchg_put(const XchgSite& x, int N, int rt, i
 // R re-read entry R - 1) and only then tests them: a load behind a runtime `t < R` branch made the
 // compiler wait for each load on its own (vmcnt(0) per entry: R dependent round trips per sweep,
 // ~3 us per exchange at R = 4), a straight run waits once per sweep.
+// Entries t0 .. t0 + NR - 1 (those < R) into a[t], b[t] (t relative to t0).
 template <int NR>
 __device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, int col, unsigned tag,
-                                               float (&a)[NR], float (&b)[NR], int trace_rt) {
+                                               float (&a)[NR], float (&b)[NR], int trace_rt, int t0 = 0) {
   const __amdgpu_buffer_rsrc_t rn = p3d_rsrc(x.near), rs = p3d_rsrc(x.slots);
 #ifdef P3D_TRACE
   const int tix = (col >> 4) + (N >> 4) * trace_rt;
@@ -173,14 +176,16 @@ __device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, 
 #endif
   bool got[NR];
 #pragma unroll
-  for (int t = 0; t < NR; ++t) got[t] = t >= R;
+  for (int t = 0; t < NR; ++t) got[t] = t0 + t >= R;
   for (int spin = 0;; ++spin) {
     const bool far_sweep = (spin & 7) == 7;   // every 8th sweep: a sibling on another XCD (sc1 copy)
     const __amdgpu_buffer_rsrc_t rr = far_sweep ? rs : rn;
     u32x4_t v[NR];
 #pragma unroll
-    for (int t = 0; t < NR; ++t)
-      v[t] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, ((t < R ? t : R - 1) * N + col) * 16, 0, 16));
+    for (int t = 0; t < NR; ++t) {
+      const int e = t0 + t < R ? t0 + t : R - 1;
+      v[t] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, (e * N + col) * 16, 0, 16));
+    }
     bool ok = true;
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
@@ -214,33 +219,71 @@ __device__ __forceinline__ void p3d_xchg_get_n(const XchgSite& x, int N, int R, 
 // run 4 iterations, not 16 guarded ones -- 16 guarded Chan terms, each with its divide, had
 // cost ~0.5 us per forward launch).  Forward: the batch mean / variance (Chan, row-tile order);
 // backward: sum g, sum g xhat (row-tile order).  Same association as the split kernels.
-template <int NR>
+// CH < NR (16-wave kernels, see p3d_xchg_sums): two passes over the entries in rounds of CH -- the
+// sum (then the mean), then the Chan terms -- the same association as one pass over all NR.  The
+// second pass re-reads entries that are already tagged (a slot is re-tagged only by the next launch
+// of the site, stream-ordered behind this one): its sweeps match at once.
+template <int NR, int CH = NR>
 __device__ __forceinline__ void p3d_xchg_moments(const XchgSite& x, int N, int R, int col, unsigned tag, int rt,
                                                  int M, float& mean, float& var) {
-  float st[NR], qt[NR];
-  p3d_xchg_get_n<NR>(x, N, R, col, tag, st, qt, rt);
-  float S = 0.f;
-#pragma unroll
-  for (int t = 0; t < NR; ++t)
-    if (t < R) S += st[t];
+  static_assert(NR % CH == 0, "p3d_xchg_moments: NR must be a multiple of CH");
   const float fm = (float)M;
-  mean = S / fm;
-  float M2 = 0.f;
+  if constexpr (CH == NR) {
+    float st[NR], qt[NR];
+    p3d_xchg_get_n<NR>(x, N, R, col, tag, st, qt, rt);
+    float S = 0.f;
 #pragma unroll
-  for (int t = 0; t < NR; ++t)
-    if (t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, M - 16 * t), mean);
-  var = M2 / fm;
+    for (int t = 0; t < NR; ++t)
+      if (t < R) S += st[t];
+    mean = S / fm;
+    float M2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+      if (t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, M - 16 * t), mean);
+    var = M2 / fm;
+  } else {
+    float S = 0.f;
+#pragma unroll
+    for (int c0 = 0; c0 < NR; c0 += CH) {
+      if (c0 >= R) break;
+      float st[CH], qt[CH];
+      p3d_xchg_get_n<CH>(x, N, R, col, tag, st, qt, rt, c0);
+#pragma unroll
+      for (int t = 0; t < CH; ++t)
+        if (c0 + t < R) S += st[t];
+    }
+    mean = S / fm;
+    float M2 = 0.f;
+#pragma unroll
+    for (int c0 = 0; c0 < NR; c0 += CH) {
+      if (c0 >= R) break;
+      float st[CH], qt[CH];
+      p3d_xchg_get_n<CH>(x, N, R, col, tag, st, qt, rt, c0);
+#pragma unroll
+      for (int t = 0; t < CH; ++t)
+        if (c0 + t < R) M2 += p3d_chan_term(st[t], qt[t], min(16, M - 16 * (c0 + t)), mean);
+    }
+    var = M2 / fm;
+  }
 }
-template <int NR>
+// CH < NR: the entries in rounds of CH, each round summed (in row-tile order, so the same bits)
+// before the next is fetched -- 16-wave kernels have 128 registers per lane, and 16 entries held
+// at once spilled 64 of them to scratch (round 5, tools/kdev.hip).
+template <int NR, int CH = NR>
 __device__ __forceinline__ void p3d_xchg_sums(const XchgSite& x, int N, int R, int col, unsigned tag, int rt,
                                               float& sa, float& sb) {
-  float at[NR], bt[NR];
-  p3d_xchg_get_n<NR>(x, N, R, col, tag, at, bt, rt);
+  static_assert(NR % CH == 0, "p3d_xchg_sums: NR must be a multiple of CH");
   sa = 0.f;
   sb = 0.f;
 #pragma unroll
-  for (int t = 0; t < NR; ++t)
-    if (t < R) { sa += at[t]; sb += bt[t]; }
+  for (int c0 = 0; c0 < NR; c0 += CH) {
+    if (c0 >= R) break;                                   // (wave-uniform)
+    float at[CH], bt[CH];
+    p3d_xchg_get_n<CH>(x, N, R, col, tag, at, bt, rt, c0);
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (c0 + t < R) { sa += at[t]; sb += bt[t]; }
+  }
 }
 
 // Row tile 0 of column tile ct, after its swap: the tile's next launch gets a new tag.

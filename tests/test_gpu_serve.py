@@ -364,7 +364,9 @@ def test_serve6_late_xcd_group_keeps_launch_epochs(monkeypatch, xcc):
     advanced the epoch at the end of workgroup 0's work, so a whole XCD group that started after
     workgroup 0 had finished (possible with max_groups = 1: workgroup 0 often idles) read the next
     epoch, ran on the other bank and left its flags there -- the NEXT launch's hand-offs then passed
-    on stale flags.  Now the last workgroup to arrive advances the epoch.  Test hook
+    on stale flags.  Now every group slot has its own epoch word, read by each member at its start
+    and advanced by the group's rank-0 member at the end of its work (by then every member has read
+    it: rank 0's waves waited for a flag of every member, posted after that read).  Test hook
     P3D_SERVE_TEST_DELAY=n,xcc: on every other call all workgroups of XCD xcc start ~n x 3.4 us
     late; the launches alternate delayed / on time and every output must equal an undelayed
     model's bits."""

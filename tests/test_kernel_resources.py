@@ -29,6 +29,9 @@ HOT = [
     "k_wgrad_multi",                      # cfg3 weight gradients + fused TF1 Adam
     "k_adam_pack",                                    # DP optimizer
     "void k_fwd<1, 8, 8, 2, true, true, 1>(FwdArgs)",  # BN-train hidden forward (exchange form)
+    "void k_dgrad<1, 16, 4, 2, true, 1>",             # hidden data gradient (16 waves, default)
+    "void k_fwd<1, 16, 4, 2, true, false, 2>",        # inference output layer (16 waves split K)
+    "void k_fwd<1, 16, 4, 2, true, true, 1>",
     "void k_gemm_f32<2, 2, true>",                    # cfg4 large-M hidden layer
     "void k_gemm_f32<2, 2, false>",                   # cfg4 large-M input layer
 ]
