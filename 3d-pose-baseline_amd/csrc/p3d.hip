@@ -135,6 +135,8 @@ struct p3d_model {
   unsigned short* abf = nullptr;    // bf16 packed activations, one slab per layer (+ x slab)
   int64_t Mpad128 = 0;
   int bf16_stages = 48;             // hidden bf16 GEMM form (launch_bf16_layer; env P3D_BF16_STAGES: 48, 0)
+  int bf16_direct = 0;              // hidden bf16 layers as k_gemm_bf16d (K split over the waves, operands
+                                    // straight into registers; env P3D_BF16_DIRECT)
   int bf16_split = 0;               // hidden bf16 layers as k_gemm_bf16s (256 x 128 tiles, K split in two
                                     // halves that meet in the launch) where M % 256 == 0 (env P3D_BF16_SPLIT=1;
                                     // measured 43.9 vs 44.6 us in step order, 42.5 vs 39.0 us hot: opt-in)
@@ -197,6 +199,7 @@ struct p3d_model {
   // persistent XCD-local evaluation (p3d_serve): per-XCD activation slabs, output partials,
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
+  float* serve6_act = nullptr;   // k_serve6's activation slabs (4 per group, P3D_SERVE6_ROWS rows in all)
   float* serve_ecg = nullptr;      // k_serve6 epilogue-constant table (k_serve_prep), [layer][tile][48] + divisors
   bool serve_ec_dirty = true;      // parameters or moving statistics changed since the table was formed
   unsigned* serve_sync = nullptr;  // [k_serve6 bank 0 | bank 1 | k_serve5 bank | device epoch word ...]
@@ -308,6 +311,7 @@ void free_all(p3d_model* m) {
   if (m->aff) (void)hipFree(m->aff);
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
+  if (m->serve6_act) (void)hipFree(m->serve6_act);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
   if (m->serve_ecg) (void)hipFree(m->serve_ecg);
   if (m->bf16s_part) (void)hipFree(m->bf16s_part);
@@ -663,6 +667,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     m->Mpad128 = (c.max_batch + 127) / 128 * 128;
     if (const char* ev = getenv("P3D_BF16_STAGES")) m->bf16_stages = atoi(ev);
     if (const char* ev = getenv("P3D_BF16_SPLIT")) m->bf16_split = atoi(ev);
+    if (const char* ev = getenv("P3D_BF16_DIRECT")) m->bf16_direct = atoi(ev);
     const int64_t slab = m->Mpad128 * L;  // bf16 elements per activation slab
     if ((e = hipMalloc(&m->wbf, nbf * 2)) != hipSuccess) return cleanup(e);
     if ((e = hipMemset(m->wbf, 0, nbf * 2)) != hipSuccess) return cleanup(e);
@@ -1018,6 +1023,13 @@ static int launch_bf16_layer(p3d_model* m, int l, int Mp, hipStream_t st) {
     m->bf16_kname = "k_gemm_bf16s<3>";
     go(ps, k_gemm_bf16s<3>, dim3((unsigned)(2 * T)), dim3(512), st, sa);
     LAUNCH_CHECK("k_gemm_bf16s");
+    return P3D_OK;
+  }
+  if (l > 0 && m->bf16_direct && Mp % 128 == 0 && ly.N % 128 == 0 && ly.K % 256 == 0) {
+    ProfScope ps(m, "bf16_hidden");
+    m->bf16_kname = "k_gemm_bf16d<2>";
+    go(ps, k_gemm_bf16d<2>, dim3(grid), dim3(256), st, a);
+    LAUNCH_CHECK("k_gemm_bf16d");
     return P3D_OK;
   }
   // hidden layers: k_gemm_bf16p<64, 4, 8> (default), the unpipelined k_gemm_bf16<64, 4>
@@ -1519,6 +1531,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     plan = serve6_plan(m, B, L / 16);
     a.split = plan.S;
     use6 = plan.S > 0;                       // no form covers this width: k_serve5
+    // k_serve6's four activation slabs per group (8 S groups of 16 RT rows) in serve6_act
+    if (use6 && (int64_t)8 * plan.S * 16 * plan.rt > P3D_SERVE6_ROWS) use6 = false;
     if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
   }
   a.ecg = m->serve_ecg;
@@ -1544,7 +1558,14 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   }
   // (k_serve6 picks its bank from the device epoch word: no memset in front, graph replays
   // alternate the banks by themselves)
+  if (use6 && !m->serve6_act) {
+    const int64_t n6 = (int64_t)4 * P3D_SERVE6_ROWS * L;
+    if ((e = hipMalloc(&m->serve6_act, n6 * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+  }
   if (use6) {
+    a.act = m->serve6_act;                   // [group][4 slabs][16 RT rows][L]; no output partials
+    a.part = nullptr;
     const int T = L / 16;
     const int ncm = plan.ncm;
     int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;

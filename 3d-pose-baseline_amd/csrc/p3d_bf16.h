@@ -345,6 +345,126 @@ __global__ __launch_bounds__(64 * WAVES) void k_gemm_bf16p(GemmBf16Args p) {
   }
 }
 
+typedef unsigned p3d_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_bf16s_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+// =====================================================================================
+// K split over the 4 waves of a 128 x 128 tile, operands loaded straight into registers
+// (k_gemm_bf16d, round 5).
+//
+// Why: k_gemm_bf16p is bound by its operand intake -- 2 MB per CU per layer through LDS-DMA,
+// whose per-CU rate tops out near 70 GB/s; the PMC pass of the cfg5 step put the CU's texture
+// addresser (TA) busy 0.76 of the kernel (profiles/r05_v1_pmc_units_stress.json) against MFMA
+// busy 0.27.  Register loads of hand-off data reach ~110-120 GB/s per CU (MI355X_MICROARCH.md,
+// handoff-payload).  Splitting the tile's K over the waves (not its rows or columns) keeps every
+// operand byte loaded ONCE per CU: wave w takes k-groups [ngA w / 4, ngA (w+1) / 4) of all 8 row
+// tiles and all 8 column tiles -- per k-group 16 fragments (16 KB) for 64 MFMAs into a 128 x 128
+// fp32 accumulator (256 AGPRs at one wave per SIMD, 512 registers), the next D - 1 k-groups' 16
+// fragments in flight (a D-deep register ring).  The four K-slice sums meet in LDS as
+// ((s0 + s2) + (s1 + s3)) -- one fixed association -- then the fused epilogue of k_gemm_bf16p.
+// =====================================================================================
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm_bf16d(GemmBf16Args p) {
+  constexpr int ES = 132;                                    // fp32 tile row stride in LDS
+  __shared__ __attribute__((aligned(16))) float red[2 * 128 * ES];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tiles_n = p.N / 128, tiles_m = p.M / 128;
+  const int GM = (tiles_m % 4 == 0) ? 4 : ((tiles_m % 2 == 0) ? 2 : 1);
+  const int grp = tile_id / (GM * tiles_n), in_grp = tile_id % (GM * tiles_n);
+  const int mt = grp * GM + (in_grp % GM), nt = in_grp / GM;
+  const int ngA = p.K / 32;
+  const int kb = (ngA * w) >> 2, nk = ((ngA * (w + 1)) >> 2) - kb;   // this wave's k-groups (nk % D == 0)
+  const __amdgpu_buffer_rsrc_t ra = p3d_bf16s_rsrc((const unsigned char*)p.A + (int64_t)(8 * mt) * ngA * 1024);
+  const __amdgpu_buffer_rsrc_t rb = p3d_bf16s_rsrc((const unsigned char*)p.Bt + (int64_t)(8 * nt) * ngA * 1024);
+  const int voff = lane * 16;
+  bf16x8 fa[D][8], fb[D][8];
+  auto load = [&](int d, int g) {   // k-group kb + g of all 8 row tiles and all 8 column tiles
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      fa[d][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, (j * ngA + kb + g) * 1024, 0));
+      fb[d][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, voff, (j * ngA + kb + g) * 1024, 0));
+    }
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfmas = [&](int d) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[d][r], fb[d][c], acc[r][c], 0, 0, 0);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, d);
+  for (int g0 = 0; g0 < nk - D; g0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      mfmas(d);
+      load(d, g0 + D + d);
+      __builtin_amdgcn_sched_barrier(0);    // the refill of slot d stays ahead of slot d + 1's MFMAs
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) mfmas(d);
+  // ---- K slices: waves 2, 3 hand theirs to waves 0, 1 (s0 + s2, s1 + s3), then both halves ----
+  const int i = lane & 15, q = lane >> 4;
+  auto put = [&](float* et) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) et[(16 * r + 4 * q + e) * ES + 16 * c + i] = acc[r][c][e];
+  };
+  if (w >= 2) put(red + (w - 2) * 128 * ES);
+  __syncthreads();
+  if (w < 2) {                               // in place: half w = s_w + s_(w+2)
+    float* et = red + w * 128 * ES;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = (16 * r + 4 * q + e) * ES + 16 * c + i;
+          et[k] = acc[r][c][e] + et[k];
+        }
+  }
+  __syncthreads();
+  // ---- epilogue (k_gemm_bf16p's): element = half 0 + half 1, bias / BN / ReLU / residual ----
+  const int ngY = p.N / 32;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int item = it * 256 + tid;
+    const int chunk = item >> 6, l = item & 63;
+    const int rl = 16 * (chunk >> 2) + (l & 15);
+    const int cl = 32 * (chunk & 3) + 8 * (l >> 4);
+    const int row = 128 * mt + rl, col = 128 * nt + cl;
+    const int64_t off = p3d_pk16(row, col, ngY);
+    u16x8 rv;
+    if (p.res) rv = *(const u16x8*)(p.res + off);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int n = col + e;
+      const float s = red[rl * ES + cl + e] + red[128 * ES + rl * ES + cl + e];
+      float z = s + p.epi.bias[n];
+      float y = p.epi.inv ? z * p.epi.inv[n] + p.epi.shift[n] : z;
+      if (p.epi.relu) y = fmaxf(y, 0.0f);
+      if (p.res) y += p3d_bf2f(rv[e]);
+      o[e] = p3d_f2bf(y);
+    }
+    *(u16x8*)(p.Y + off) = o;
+  }
+}
+
 // =====================================================================================
 // Split-K form for wide layers at modest M (cfg5: M = 1024, N = K = 4096).
 //
@@ -371,10 +491,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_gemm_bf16p(GemmBf16Args p) {
 // has a lower workgroup id than every reader, so the dispatcher places all writers before any
 // reader, and writers wait for nothing.  The poll is bounded and reports through *err.
 // =====================================================================================
-typedef unsigned p3d_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_bf16s_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
 // 16-B sc1 load (L1 bypassed): the partial another workgroup stored write-through
 __device__ __forceinline__ f32x4 p3d_bf16s_ld(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));

@@ -1086,9 +1086,14 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
 template <bool NOADAM = false>
 __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
   P3D_WG_STAMP(0);
-  constexpr int XS = NOADAM ? 64 * 64 : 64 * WG_LDS_STRIDE;
-  __shared__ __attribute__((aligned(16))) float xs[XS];
-  __shared__ __attribute__((aligned(16))) float zs[XS];
+  // both forms use the swizzled 16 KB operand images (round 5: the fused form too -- 33 KB of
+  // LDS instead of 41 KB, so 4 workgroups fit on a CU and cfg3's 1,024 hidden-layer tiles run in
+  // one round instead of 768 + 256); one array, so the fused Adam's 64 x 65 transpose tile
+  // (16.6 KB) can run over into the dead dZ image
+  constexpr int XS = 64 * 64;
+  __shared__ __attribute__((aligned(16))) float xz[2 * XS];
+  float* xs = xz;
+  float* zs = xz + XS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
   const int n0 = bx * 64, k0 = by * 64;
@@ -1105,26 +1110,26 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
     Stage64 sx, sz;
     p3d_stage64_load(sx, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
     p3d_stage64_load(sz, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
-    p3d_stage64_store<NOADAM>(xs, sx, p.xpk);
-    p3d_stage64_store<NOADAM>(zs, sz, p.zpk);
+    p3d_stage64_store<true>(xs, sx, p.xpk);
+    p3d_stage64_store<true>(zs, sz, p.zpk);
     __syncthreads();
     P3D_WG_STAMP(1);
 #pragma unroll NOADAM ? 2 : 4
     for (int t = 0; t < 16; ++t) {
       const int m = 4 * t + q;
-      const float a = xs[p3d_wg_lidx<NOADAM>(m, 16 * w + i)];
+      const float a = xs[p3d_wg_lidx<true>(m, 16 * w + i)];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[p3d_wg_lidx<NOADAM>(m, 16 * s + i)], acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, zs[p3d_wg_lidx<true>(m, 16 * s + i)], acc[s], 0, 0, 0);
     }
     if (do_db) {
       if (NOADAM) {   // (the same sums, fewer registers live)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dbs += zs[p3d_wg_lidx<NOADAM>(16 * w + r, lane)];
+        for (int r = 0; r < 16; ++r) dbs += zs[p3d_wg_lidx<true>(16 * w + r, lane)];
       } else {
         float v[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = zs[p3d_wg_lidx<NOADAM>(16 * w + r, lane)];
+        for (int r = 0; r < 16; ++r) v[r] = zs[p3d_wg_lidx<true>(16 * w + r, lane)];
 #pragma unroll
         for (int r = 0; r < 16; ++r) dbs += v[r];
       }
@@ -1260,7 +1265,7 @@ __device__ __forceinline__ void p3d_wgrad_multi_body(const WgradMulti& mw) {
     st->global_step = st->global_step + 1;
   }
 }
-__global__ __launch_bounds__(256) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
+__global__ __launch_bounds__(256, 4) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
 // the gradient-only form, 4 workgroups (4 waves per SIMD) per CU (see p3d_wgrad_tile)
 __global__ __launch_bounds__(256, 4) void k_wgrad_grad(WgradMulti mw) { p3d_wgrad_multi_body<true>(mw); }
 

@@ -63,6 +63,7 @@
 // k_serve6's 64 per-group-slot epoch words (bank = epoch & 1)
 #define P3D_SERVE_SYNC_ALL (3 * P3D_SERVE_SYNC_WORDS + 64)
 #define P3D_SERVE_GROUPS 32        // XCD groups (k_serve5 SPLIT = 4: four per XCD)
+#define P3D_SERVE6_ROWS 4096       // k_serve6: rows in flight (8 S groups x 16 RT rows) its slabs hold
 #define P3D_SERVE_SPIN (1 << 22)   // bounded spins (~0.5 s): a stuck group reports instead of hanging
 #ifndef P3D_SERVE_SLICE_WAIT       // k_serve5: each wave waits only for the members its K slice reads
 #define P3D_SERVE_SLICE_WAIT 1

@@ -26,13 +26,19 @@
 //     contiguous tiles [T r / n, T (r+1) / n) (T = L / 16), i.e. floor or ceil of T / n, and
 //     contracts them (all 4 row tiles) as one contraction of NCM tiles (a member with fewer
 //     computes a copy of its last tile and stores nothing for it; one with more loops);
-//   * the fused output layer writes one 64 x 48 partial per column tile, and a step's output is
-//     their sum in a fixed association (4 slices of T/4 tiles in order, then the slices in
-//     order) -- independent of n and S, so every launch shape gives the same bits.
+//   * the output layer is a phase of its own (round 5; it was fused into the last hidden epilogue
+//     as one 64 x 48 partial per column tile, summed by a reduction: 15.7 MB of partials per
+//     20-step launch and a full-group wait): its RT x NDT tiles are dealt over the members and
+//     contracted like hidden tiles, K split over the 4 waves, slices summed in order -- the
+//     association is fixed by the tile, independent of n and S, so every launch shape gives the
+//     same bits.
 #pragma once
 #include "p3d_serve.h"
 
-#define P3D_SERVE6_RE 2            // output-reduction elements per lane (E4 / n <= 128)
+#ifndef P3D_S6_LATE_EPOCH
+#define P3D_S6_LATE_EPOCH 1        // the epoch read off the prologue's critical path (round 5)
+#endif
+
 
 // Timeline stamps for development (-DP3D_TRACE, tools/trace_serve6.py): for every group, its
 // rank-0 member (row 0) and its first member with the most tiles (row 1), first step only:
@@ -88,11 +94,9 @@ __device__ __forceinline__ int p3d_tile_owner(int t, int n, int T) { return ((t 
 template <int DEPTH, int NDT, int NCM, int RT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve6(ServeArgs p) {
   static_assert(RT >= 1 && RT <= 16, "row tiles per unit");
-  constexpr int RE = P3D_SERVE6_RE;
   constexpr int ROWS = 16 * RT;              // rows of one unit
   constexpr int UMAX = (RT * NCM + 3) / 4;   // 16 x 16 tiles a wave finishes per chunk
-  constexpr int PT = RT * NDT * 256;         // floats of one tile's output partial
-  constexpr int E4 = RT * NDT * 64;          // float4 elements of a unit's output
+  constexpr int OCH = RT * NCM < 4 ? RT * NCM : 4;   // output tiles per round of the output phase
   // activation ring depth (the wide forms cannot hold both rings DEPTH deep: 4 x 11 fragments
   // spilled 77 registers at NCM = 7, RT = 4)
   constexpr int DA = RT >= 6 ? (DEPTH >= 8 ? 4 : 2) : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);
@@ -102,7 +106,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int PD = P3D_S6_PD;
 #endif
   __shared__ __attribute__((aligned(16))) f32x4 red[4 * RT * NCM * 64];  // [slice][rt][tile][lane]
-  __shared__ __attribute__((aligned(16))) f32x4 rsum[4 * 64 * RE];       // split output reduction
   // epilogue constants of the member's tiles (up to ECT of them), per layer 0..2N:
   // bias | inv | shift, and each layer's max-norm divisor.  Every epilogue reads them from
   // LDS: no global load on a branch of the epilogue, so the compiler's vmcnt waits there stay
@@ -220,6 +223,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // workgroup 0 had finished -- an idle one at max_groups = 1 -- read the advanced epoch, ran on the
   // other bank and left its flags there for the next launch; one launch-wide arrival counter
   // instead cost 2-3 us per launch: 256 returning atomics on one word, serialised.)
+#if P3D_S6_LATE_EPOCH
+  // (round 5) the epoch is needed first at the input layer's hand-off: read behind the first
+  // unit's operands, kept by thread 0 until the first group_sync parks it in LDS -- its memory
+  // round trip (the word was last written by an atomic) overlaps the constants and the input
+  // layer instead of holding a barrier in front of them
+  prefetch(gi, (T * r) / n, (T * (r + 1)) / n);
+  if (tid == 0 && placeable) ep = __hip_atomic_load(p.epoch + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
   if (tid == 0 && placeable) ep = __hip_atomic_load(p.epoch + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the first unit's input-layer operands and the epilogue constants in flight with the epoch read
   prefetch(gi, (T * r) / n, (T * (r + 1)) / n);
@@ -231,6 +242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     sh[5] = (placeable && r == 0 && gi >= 0 && gi < p.nb) ? gid : -1;
   }
   __syncthreads();
+#endif
 #ifdef P3D_TRACE
   if (tid == 0 && blockIdx.x < 1024) {     // per workgroup: start, placement known, XCD | rank
     g_p3d_trace[16384 + blockIdx.x * 4 + 0] = t_start;
@@ -239,13 +251,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     g_p3d_trace[16384 + blockIdx.x * 4 + 3] = (unsigned long long)(xcc | (rx << 8) | (sh[0] << 16));
   }
 #endif
-  const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
-  unsigned* sync = p.sync + bank * P3D_SERVE_SYNC_WORDS;
   // the group's flags in the other bank, zeroed for the group's next launch (every member the same
   // 64 words; nothing of this launch uses that bank).  Invariant: at the start of a launch the bank
   // of a group slot's epoch holds zeros (an idle group posts nothing and does not advance).
-  if (placeable && tid < 64) p.sync[(bank ^ 1) * P3D_SERVE_SYNC_WORDS + P3D_SERVE_FLAG0 + 64 * gid + tid] = 0u;
-  if (sh[2]) {
+  unsigned* flags = nullptr;                 // this launch's bank (bind_bank)
+  auto bind_bank = [&]() {                   // after a barrier that published sh[3]
+    const int bank = __builtin_amdgcn_readfirstlane(sh[3]);
+    flags = p.sync + bank * P3D_SERVE_SYNC_WORDS + P3D_SERVE_FLAG0 + 64 * gid;
+    if (placeable && tid < 64) p.sync[(bank ^ 1) * P3D_SERVE_SYNC_WORDS + P3D_SERVE_FLAG0 + 64 * gid + tid] = 0u;
+  };
+#if !P3D_S6_LATE_EPOCH
+  bind_bank();
+#endif
+  const bool bad_launch = (gridDim.x & 7u) != 0u || p.split < 1 || p.split > 8 || p.census_extra;
+  if (bad_launch) {
     // a placement this launch cannot use: no row of it is computed by this workgroup; it fills
     // a stripe of the output with NaN, so a caller who skips p3d_serve_check / p3d_error_flags
     // never reads a stale or unwritten row as a result (the error word is set)
@@ -256,10 +275,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tid == 0) __hip_atomic_store(p.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     gi = p.nb;                               // the whole group reports instead of computing
   }
-  unsigned* flags = sync + P3D_SERVE_FLAG0 + 64 * gid;   // (this launch's bank)
   const int64_t slab = (int64_t)ROWS * L;
-  float* act = p.act + (int64_t)gid * 3 * slab;
-  float* part = p.part + (int64_t)gid * 2 * T * PT;
+  // slabs 0..2: the hidden layers' rotation; slab 3: the last hidden layer's output, the output
+  // layer's input (the next step's input layer writes the slab of the rotation the last phase reads
+  // nothing from, so the last phase's output needs a fourth)
+  float* act = p.act + (int64_t)gid * 4 * slab;
   const ServeLayer& li = p.ly[0];
   const ServeLayer& lo = p.ly[2 * p.nblk + 1];
   const bool wsq_any = li.wsq != nullptr;
@@ -268,8 +288,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   bool broken = false;
   const int gb = (ngL * w) >> 2, gcount = ngL >> 2;      // this wave's K slice (k-groups)
   const int t_lo = (T * r) / n, t_hi = (T * (r + 1)) / n; // this member's column tiles
-  // this member's share of a step's output elements (split reduction: <= 64 RE per member)
-  const int es = (int)(((int64_t)E4 * r) / n), ecnt = (int)(((int64_t)E4 * (r + 1)) / n) - es;
 #ifdef P3D_TRACE
   {
     const int ncmax = (T + n - 1) / n;
@@ -278,7 +296,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (tr6 && tid == 0) { tr6[0] = t_start; tr6[1] = wall_clock64(); }
   }
 #endif
-  const bool split_red = t_lo < t_hi && ecnt <= 64 * RE;
 
   bool trs = true;                           // stamping this step (the group's first)
   // input layer of the chunk at c0 for the unit at rbase: this wave's tiles (unit j: row tile
@@ -337,7 +354,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto group_sync = [&](bool full) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (broken) sh[4] = 1;
+#if P3D_S6_LATE_EPOCH
+    const bool first = flags == nullptr;
+    if (first && tid == 0) {
+      sh[3] = (int)(ep & 1u);
+      // the epoch word this workgroup advances at its end (-1: none), parked in LDS: kept in
+      // registers across the whole launch it cost the main loop its register allocation (222 vs
+      // 166 AGPRs, 134 vs 113 us per launch)
+      sh[5] = (placeable && r == 0 && gi >= 0 && gi < p.nb) ? gid : -1;
+    }
     __syncthreads();
+    if (first) bind_bank();
+#else
+    __syncthreads();
+#endif
     broken = broken || sh[4] != 0;           // workgroup-wide from here (monotonic)
     ++nsync;
     if (tid == 0)
@@ -391,65 +421,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  // output of the step at row0 from its T tile partials: member's elements [es, es + ecnt),
-  // wave w sums slice w (tiles [T w / 4, T (w+1) / 4)) in tile order into LDS; red_store adds
-  // the four slices in slice order (after the caller's __syncthreads)
-  // the same sums with every partial requested before the first add (16 tiles per slice in
-  // flight: the launch's last reduction, nothing else is live then)
-  // every load of a 16-tile chunk, for all RE elements, issued before the first add (clamped
-  // addresses, no branch around a load: one round of L2 latency per chunk, not one per element)
-  auto red_slices_all = [&](const float* pb) {
-    const __amdgpu_buffer_rsrc_t rp = p3d_rsrc(pb);
-    const int tb = (T * w) >> 2, te = (T * (w + 1)) >> 2;
-    f32x4 ss[RE];
-#pragma unroll
-    for (int j = 0; j < RE; ++j) ss[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t0 = tb; t0 < te; t0 += 16) {
-      f32x4 v[RE][16];
-#pragma unroll
-      for (int j = 0; j < RE; ++j) {
-        const int el = lane + 64 * j, elc = el < ecnt ? el : 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[j][k] = p3d_ld_sc1(rp, (min(t0 + k, te - 1) * E4 + es + elc) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < RE; ++j) {
-        ss[j] = t0 == tb ? v[j][0] : ss[j] + v[j][0];
-#pragma unroll
-        for (int k = 1; k < 16; ++k)
-          if (t0 + k < te) ss[j] += v[j][k];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < RE; ++j) {
-      const int el = lane + 64 * j;
-      rsum[w * 64 * RE + el] = el < ecnt ? ss[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
   const float qnan = __builtin_nanf("");
-  auto red_store = [&](int64_t prow0) {      // after a __syncthreads
-    if (tid < ecnt) {
-      f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The output layer of the step at orow0 (round 5: its own phase instead of per-tile partials
+  // summed by a reduction): the unit's RT x NDT output tiles are dealt contiguously over the
+  // members; each tile is contracted over K = L as every hidden tile is -- wave w the k-groups of
+  // its K slice, one MFMA chain in k-group order (A = the last hidden layer's output fragment, B =
+  // the W4 fragment), then the four slices summed in slice order -- so the association is fixed by
+  // the tile and every launch form gives the same bits.  Reads slab 3 after the last phase's
+  // hand-off (this wave's K-slice producers); nothing is written but y.
+  auto out_phase = [&](int64_t orow0) {
+    constexpr int OT = RT * NDT;
+    const int o_lo = (OT * r) / n, o_hi = (OT * (r + 1)) / n;
+    const __amdgpu_buffer_rsrc_t ry = p3d_rsrc(act + 3 * slab), r4 = p3d_rsrc(lo.Wf);
+    for (int c0 = o_lo; c0 < o_hi; c0 += OCH) {
+      const int nt = min(OCH, o_hi - c0);
+      f32x4 oacc[OCH];
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 * RE + tid];
-      if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
-      p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prow0);
-    }
-  };
-  // non-split form (large T or small groups): same association, thread per element
-  auto red_plain = [&](const float* pb, int64_t prow0) {
-    const __amdgpu_buffer_rsrc_t rs = p3d_rsrc(pb);
-    for (int e4 = es + tid; e4 < es + ecnt; e4 += 256) {
-      f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int sl = 0; sl < 4; ++sl) {
-        const int tb = (T * sl) >> 2, te = (T * (sl + 1)) >> 2;
-        if (tb == te) continue;
-        f32x4 ss = p3d_ld_sc1(rs, (tb * E4 + e4) * 16);
-        for (int t = tb + 1; t < te; ++t) ss += p3d_ld_sc1(rs, (t * E4 + e4) * 16);
-        sum += ss;
+      for (int j = 0; j < OCH; ++j) oacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < OCH; ++j) {
+        if (j >= nt) break;                    // (workgroup-uniform)
+        const int tile = c0 + j, ort = tile / NDT, oo = tile % NDT;
+        // the K slice in halves of 8 k-groups, both halves' fragments requested before the first
+        // MFMA (32 loads at L = 1024: the hidden rings are dead here; two 8-entry arrays stay in
+        // registers where one 16-entry array went to scratch)
+        constexpr int GH = 8;
+        auto ld_half = [&](int gs, f32x4 (&av)[GH], f32x4 (&wv)[GH]) {
+#pragma unroll
+          for (int g = 0; g < GH; ++g) {
+            const int gg = gb + min(gs + g, gcount - 1);
+            av[g] = p3d_ld_sc1(ry, ((ort * ngL + gg) * 64 + lane) * 16);
+            wv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r4, ((oo * ngL + gg) * 64 + lane) * 16, 0, 0));
+          }
+        };
+        auto mma_half = [&](int gs, const f32x4 (&av)[GH], const f32x4 (&wv)[GH]) {
+#pragma unroll
+          for (int g = 0; g < GH; ++g) {
+            if (gs + g >= gcount) break;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) oacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][e], wv[g][e], oacc[j], 0, 0, 0);
+          }
+        };
+        for (int g0 = 0; g0 < gcount; g0 += 2 * GH) {
+          f32x4 a0[GH], w0[GH], a1[GH], w1[GH];
+          ld_half(g0, a0, w0);
+          ld_half(g0 + GH, a1, w1);
+          mma_half(g0, a0, w0);
+          mma_half(g0 + GH, a1, w1);
+        }
       }
-      if (broken) sum = f32x4{qnan, qnan, qnan, qnan};
-      p3d_serve_store_out<NDT>(p, lo, sum, e4, prow0);
+#pragma unroll
+      for (int j = 0; j < OCH; ++j) red[(w * OCH + j) * 64 + lane] = oacc[j];
+      __syncthreads();
+      if (w < nt) {                            // wave j sums tile j's four slices in slice order
+        f32x4 tot = red[(0 * OCH + w) * 64 + lane];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) tot += red[(k * OCH + w) * 64 + lane];
+        if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
+        p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
+      }
+      __syncthreads();                         // red is rewritten next (next round / phase)
     }
   };
 
@@ -465,8 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  int jl = 0, c0b = 0;
-  int64_t prev_row0 = -1;
+  int c0b = 0;
   if (gi < p.nb) {                           // the group's first step: its input layer alone
     if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, 0);
     P3D_S6_STAMP(trs, 5);
@@ -476,32 +506,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     group_sync(false);
     P3D_S6_STAMP(trs, 3);
   }
-  for (int b = gi; b < p.nb; b += ng, ++jl) {
+  for (int b = gi; b < p.nb; b += ng) {
     const int64_t row0 = (int64_t)b * ROWS;
     const bool has_next = b + ng < p.nb;
     const int c0n = (c0b + 2 * p.nblk) % 3;  // buffer the next step's input layer writes
     int cur = c0b;
-    float* pdst = part + (int64_t)(jl & 1) * T * PT;
-    const float* prev_part = part + (int64_t)((jl - 1) & 1) * T * PT;
     for (int ph = 1; ph <= NH; ++ph) {
       P3D_S6_STAMP(trs, 8 * ph);
       const bool lastp = (ph == NH);
-      const bool red_here = (ph == 1 && prev_row0 >= 0);
-      // the previous step's output (groups running several steps): before the contraction,
-      // not inside its epilogue -- loads on a branch there made the compiler's waits in the
-      // epilogue wait for every load in flight
-      if (red_here && !split_red) red_plain(prev_part, prev_row0);
-      if (red_here && split_red) {
-        red_slices_all(prev_part);
-        __syncthreads();
-        red_store(prev_row0);
-        __syncthreads();
-      }
       const ServeLayer& ly = p.ly[ph];
       const bool second = ((ph - 1) & 1) == 1;
       const int t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
       const float* A = act + (second ? t1 : cur) * slab;
-      float* Y = act + (second ? t2 : t1) * slab;
+      float* Y = act + (lastp ? 3 : (second ? t2 : t1)) * slab;
       const float* res = (second && p.residual) ? act + cur * slab : nullptr;
       const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A);
       const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024;
@@ -574,17 +591,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         P3D_S6_STAMP(trs && first_c, 8 * ph + 1);
         // the epilogue's operands first (vmcnt waits are in order: the epilogue then waits for
         // them only, not for the next ring's weights behind them)
-        // requested unconditionally (the residual operands from A where there is no residual,
-        // W4 in every phase): conditional loads would make the compiler's vmcnt waits
-        // conservative, i.e. wait for the next ring's weights behind them as well
-        f32x4 rv[UMAX], wo[UMAX][NDT];
+        // requested unconditionally (the residual operands from A where there is no residual):
+        // conditional loads would make the compiler's vmcnt waits conservative, i.e. wait for the
+        // next ring's weights behind them as well
+        f32x4 rv[UMAX];
         const __amdgpu_buffer_rsrc_t rr = p3d_rsrc(res ? res : A);
 #pragma unroll
         for (int j = 0; j < UMAX; ++j) {
           const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
           const int t = c0 + (cc < nck ? cc : nck - 1);
           rv[j] = p3d_ld_sc1(rr, (int)(((int64_t)(rt * ngL + t) * 64 + lane) * 16));
-          p3d_wo_load<NDT>(lo, t, ngL, wo[j]);
         }
         // the next contraction's first weight slots: this member's next chunk, the next
         // layer, or the next step's first layer (requested even after a group's last step:
@@ -620,17 +636,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           const int t = c0 + cc;
           f32x4 yv = epi_t(ph, t - t_lo, sacc[j]);
           if (res) yv += rv[j];
-          if (lastp) {                         // fused output layer: this tile's 64 x 48 partial
-#pragma unroll
-            for (int o = 0; o < NDT; ++o) {
-              f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(yv[e], wo[j][o][e], pacc, 0, 0, 0);
-              *(f32x4*)(pdst + (int64_t)t * PT + ((rt * NDT + o) * 64 + lane) * 4) = pacc;
-            }
-          } else {
-            *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
-          }
+          *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
         }
         P3D_S6_STAMP(trs && first_c, 8 * ph + 6);
         // red / rsum are rewritten by this member's next contraction of the phase
@@ -640,27 +646,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, c0n, t_lo);
       P3D_S6_STAMP(trs, 8 * ph + 3);
       if (second) cur = t2;
-      // after a step's last phase the output reduction reads every tile's partial: the split
-      // form reads exactly the wave's producers' (its K slice), the plain form all of them
-      group_sync(lastp && (!has_next || !split_red));
+      // every phase's hand-off: each wave waits for the members whose output its K slice reads
+      // (after the last phase: the output layer's input, slab 3, and the next step's input layer)
+      group_sync(false);
       P3D_S6_STAMP(trs, 8 * ph + 4);
     }
-    trs = false;
-    prev_row0 = row0;
-    c0b = c0n;
-  }
-  if (prev_row0 >= 0) {                      // the group's last step's output
-    const float* pb = part + (int64_t)((jl - 1) & 1) * T * PT;
-    if (split_red) {
-      red_slices_all(pb);
-      __syncthreads();
-      red_store(prev_row0);
-    } else {
-      red_plain(pb, prev_row0);
-    }
+    out_phase(row0);                         // this step's output layer
 #ifdef P3D_TRACE
-    if (tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
+    if (trs && tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
 #endif
+    trs = false;
+    c0b = c0n;
   }
   if (tid == 0 && sh[5] >= 0)   // (every member has read the epoch by now: see its read)
     __hip_atomic_fetch_add(p.epoch + sh[5], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

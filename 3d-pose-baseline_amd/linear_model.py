@@ -788,24 +788,28 @@ class LinearModel(object):
         while len(self._host_steps) >= 8:
             self._host_steps.pop(next(iter(self._host_steps)))
         f32 = torch.float32
-        st = {"hx": torch.empty((B, self.input_size), dtype=f32, pin_memory=True),
-              "ht": torch.empty((B, self.output_size), dtype=f32, pin_memory=True),
-              "hy": torch.empty((B, self.output_size), dtype=f32, pin_memory=True),
-              "hl": torch.empty(1, dtype=f32, pin_memory=True),
-              "dx": torch.empty((B, self.input_size), dtype=f32, device=self.device),
-              "dt": torch.empty((B, self.output_size), dtype=f32, device=self.device),
-              "dy": torch.empty((B, self.output_size), dtype=f32, device=self.device),
+        nx, nt, ny = B * self.input_size, B * self.output_size, B * self.output_size
+        # one pinned block per direction: [x | t] in (one H2D copy node), [y | loss] out (one D2H
+        # copy node) -- two graph copy nodes fewer per session.run than separate buffers
+        hin = torch.empty(nx + nt, dtype=f32, pin_memory=True)
+        hout = torch.empty(ny + 4, dtype=f32, pin_memory=True)
+        din = torch.empty(nx + nt, dtype=f32, device=self.device)
+        dout = torch.empty(ny + 4, dtype=f32, device=self.device)
+        st = {"hin": hin, "hout": hout, "din": din, "dout": dout,
+              "hx": hin[:nx].view(B, self.input_size), "ht": hin[nx:].view(B, self.output_size),
+              "hy": hout[:ny].view(B, self.output_size), "hl": hout[ny:ny + 1],
+              "dx": din[:nx].view(B, self.input_size), "dt": din[nx:].view(B, self.output_size),
+              "dy": dout[:ny].view(B, self.output_size), "dl": dout[ny:ny + 1],
               "graph": None}
         st["hx_np"], st["ht_np"] = st["hx"].numpy(), st["ht"].numpy()
         st["hy_np"], st["hl_np"] = st["hy"].numpy(), st["hl"].numpy()
         if not training:
             def body():
-                st["dx"].copy_(st["hx"], non_blocking=True)
-                st["dt"].copy_(st["ht"], non_blocking=True)
+                st["din"].copy_(st["hin"], non_blocking=True)
                 self.forward_device(st["dx"], False, keep, out=st["dy"])
-                loss = self.loss_device(st["dy"], st["dt"])
-                st["hy"].copy_(st["dy"], non_blocking=True)
-                st["hl"].copy_(loss, non_blocking=True)
+                check(lib().p3d_mse(ptr(st["dy"]), ptr(st["dt"]), B, self.output_size, ptr(st["dl"]), 0,
+                                    self.stream()), "p3d_mse")
+                st["hout"].copy_(st["dout"], non_blocking=True)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
@@ -817,11 +821,9 @@ class LinearModel(object):
             st["graph"] = g
         elif not self.data_parallel and os.environ.get("P3D_STEP_GRAPH", "1") != "0":
             def body():
-                st["dx"].copy_(st["hx"], non_blocking=True)
-                st["dt"].copy_(st["ht"], non_blocking=True)
-                loss, _ = self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"])
-                st["hy"].copy_(st["dy"], non_blocking=True)
-                st["hl"].copy_(loss, non_blocking=True)
+                st["din"].copy_(st["hin"], non_blocking=True)
+                self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"], loss_out=st["dl"])
+                st["hout"].copy_(st["dout"], non_blocking=True)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             g = torch.cuda.CUDAGraph()
@@ -858,11 +860,9 @@ class LinearModel(object):
                 check(lib().p3d_params_changed(self._h), "p3d_params_changed")
         else:
             lr = exponential_decay(self.lr0, self._step_host)
-            st["dx"].copy_(st["hx"], non_blocking=True)
-            st["dt"].copy_(st["ht"], non_blocking=True)
-            loss, _ = self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"])
-            st["hy"].copy_(st["dy"], non_blocking=True)
-            st["hl"].copy_(loss, non_blocking=True)
+            st["din"].copy_(st["hin"], non_blocking=True)
+            self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"], loss_out=st["dl"])
+            st["hout"].copy_(st["dout"], non_blocking=True)
         stream.synchronize()
         self.check_errors()
         lv = float(st["hl_np"][0])

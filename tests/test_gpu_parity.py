@@ -788,3 +788,40 @@ def test_set_weights_after_captured_step_keeps_every_write():
         np.testing.assert_array_equal(np.asarray(st[k]), np.asarray(v), err_msg=k)
     m.close()
     m2.close()
+
+
+@pytest.mark.parametrize("L,N,B", [(4096, 4, 1024), (512, 1, 256), (1024, 2, 128)])
+def test_bf16_direct_matches_oracle_and_single_pass(L, N, B, monkeypatch):
+    """k_gemm_bf16d (round 5: a 128 x 128 tile's K split over its 4 waves, operands loaded straight
+    into registers, slices combined as ((s0 + s2) + (s1 + s3))) vs the oracle's bf16 emulation (the
+    cfg5 tolerances of test_bf16_inference_matches_emulated_oracle) and vs k_gemm_bf16p (the same
+    values up to the fp32 association: the same bounds), bit-identical from call to call."""
+    cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
+    xn = np.random.default_rng(B + 7).standard_normal((B, 32)).astype(np.float32)
+    x = torch.from_numpy(xn).cuda()
+    ys = {}
+    for direct in ("1", "0"):
+        monkeypatch.setenv("P3D_BF16_DIRECT", direct)
+        m = linear_model.LinearModel(L, N, True, True, False, B, 1e-3, "/tmp/p3d_test", dtype="bfloat16",
+                                     seed=3, max_batch=B)
+        m.set_weights({**st.params, **st.moving})
+        y = m.forward_device(x)
+        ys[direct] = y.cpu().numpy()
+        if direct == "1":
+            import _p3d
+            name = _p3d.ctypes.create_string_buffer(128)
+            _p3d.check(_p3d.lib().p3d_kernel_name(m._h, 5, name, 128), "p3d_kernel_name")
+            assert name.value.decode() == "k_gemm_bf16d<2>", name.value
+            for _ in range(2):
+                assert torch.equal(m.forward_device(x), y)
+        m.close()
+    tmax, tmean = (1e-2, 1e-3) if L >= 1024 else (1e-3, 1e-5)
+    scale = np.abs(ys["0"]).max()
+    err = np.abs(ys["1"] - ys["0"])
+    assert err.max() <= tmax * scale and err.mean() <= tmean * scale, (err.max(), err.mean(), scale)
+    ref = ref_mlp.forward_bf16(st, xn, acc=np.float32 if L >= 4096 else np.float64)
+    tmax, tmean = (1e-2, 1e-3) if L >= 4096 else (1e-3, 1e-5)
+    scale = np.abs(ref).max()
+    err = np.abs(ys["1"] - ref)
+    assert err.max() <= tmax * scale and err.mean() <= tmean * scale, (err.max(), err.mean(), scale)
