@@ -572,6 +572,9 @@ __global__ __launch_bounds__(64 * WV) void k_gemv_fold(GemvArgs p, GemvFold f) {
 // Every wait is bounded (err); the launch needs its grid resident (host: H L / 16 <= CUs).  Same
 // k_gemv arithmetic throughout, so the same bits as the six launches
 // (tests/test_gpu_parity.py::test_gemv_small_batch).
+#ifndef P3D_CHAIN_PIN_ARGS
+#define P3D_CHAIN_PIN_ARGS 1       // k_gemv_chain's arguments fetched in one round (round 5)
+#endif
 #define P3D_GEMV_CHAIN_MAXH 8
 #define P3D_GEMV_CHAIN_MAXK 2048   // (L = 2048: the second half of each wave's slice requested after the first's FMAs)
 struct GemvChain {
@@ -613,6 +616,15 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
 #pragma unroll
   for (int k = 1; k < P3D_GEMV_CHAIN_MAXH; ++k)
     if (k == l - 1) p = c.ly[k];
+#if P3D_CHAIN_PIN_ARGS
+  // (round 5) the layer's arguments and the launch's shared ones fetched in ONE round of scalar
+  // loads: left to itself the compiler loaded them where they are used, behind branches on earlier
+  // ones -- six dependent scalar-load round trips to the argument segment the host wrote just before
+  // the launch (1.4 us to the arguments in hand, profiles/r04_chain_trace_args.json)
+  asm volatile("" ::"s"(p.Wf), "s"(p.bias), "s"(p.M), "s"(p.K), "s"(p.N), "s"(p.bn), "s"(p.relu), "s"(p.gamma),
+               "s"(p.beta), "s"(p.mmean), "s"(p.mvar), "s"(c.hand), "s"(c.err), "s"(c.res), "s"(c.T),
+               "s"(c.in.Wf), "s"(c.in.X), "s"(c.in.bias));
+#endif
   const int M = p.M, K = p.K, N = p.N, ngK = K >> 4;
   const int gb = (ngK * w) / WV, ge = (ngK * (w + 1)) / WV;
   const int col = 16 * t + i;

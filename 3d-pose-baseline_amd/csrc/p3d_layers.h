@@ -67,6 +67,9 @@ __device__ __forceinline__ float p3d_adam_alpha(const StepState* st, float lr_ho
 __device__ __forceinline__ int64_t p3d_wd_at(int k, int n, int ngd) {
   return ((int64_t)((k >> 4) * ngd + (n >> 4)) * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
 }
+// RB: rows of the thread's four requested together (4: one round trip; 2: two, 24 fewer registers
+// live -- the fused weight-gradient kernel at five workgroups per CU).
+template <int RB = 4>
 __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* g, int64_t off, int K, int N,
                                                 int k0, int n0, float* w, float* m, float* v, float* wd,
                                                 float* wf, float alpha, float omb1, float omb2, float eps,
@@ -75,41 +78,44 @@ __device__ __forceinline__ void p3d_adam_tile64(float (*tile)[65], const float* 
   const bool vec = (N & 3) == 0;
   const int ngd_ = ((N + 15) & ~15) >> 4;
   if (vec) {
+#pragma unroll
+   for (int h = 0; h < 4; h += RB) {
     // all four rows' w / m / v (and g) requested before the first update, from clamped (always
     // valid) addresses, stores after: a load inside the per-row range branch made every row a
     // dependent memory round trip (with the previous row's stores in the same wait)
-    f32x4 ww[4], mm[4], vv[4], gg[4];
-    bool ok[4];
+    f32x4 ww[RB], mm[RB], vv[RB], gg[RB];
+    bool ok[RB];
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+    for (int j = 0; j < RB; ++j) {
+      const int it = h + j, r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
       const int k = k0 + r, n = n0 + c;
-      ok[it] = k < K && n < N;
-      const int64_t base = ok[it] ? off + (int64_t)k * N + n : off;
-      ww[it] = wsrc ? *(const f32x4*)(wd + (ok[it] ? p3d_wd_at(k, n, ngd_) : 0)) : *(const f32x4*)(w + base);
-      mm[it] = *(const f32x4*)(m + base);
-      vv[it] = *(const f32x4*)(v + base);
-      if (g) gg[it] = *(const f32x4*)(g + base);
-      else gg[it] = f32x4{tile[r][c], tile[r][c + 1], tile[r][c + 2], tile[r][c + 3]};
+      ok[j] = k < K && n < N;
+      const int64_t base = ok[j] ? off + (int64_t)k * N + n : off;
+      ww[j] = wsrc ? *(const f32x4*)(wd + (ok[j] ? p3d_wd_at(k, n, ngd_) : 0)) : *(const f32x4*)(w + base);
+      mm[j] = *(const f32x4*)(m + base);
+      vv[j] = *(const f32x4*)(v + base);
+      if (g) gg[j] = *(const f32x4*)(g + base);
+      else gg[j] = f32x4{tile[r][c], tile[r][c + 1], tile[r][c + 2], tile[r][c + 3]};
     }
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
+    for (int j = 0; j < RB; ++j) {
+      const int it = h + j, r = it * 16 + (tid >> 4), c = 4 * (tid & 15);
       const int64_t base = off + (int64_t)(k0 + r) * N + n0 + c;
       float wn[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ok[it]) {
+      if (ok[j]) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float w1 = ww[it][e], m1 = mm[it][e], v1 = vv[it][e];
-          p3d_adam1(w1, m1, v1, gg[it][e], alpha, omb1, omb2, eps);
-          ww[it][e] = w1; mm[it][e] = m1; vv[it][e] = v1; wn[e] = w1;
+          float w1 = ww[j][e], m1 = mm[j][e], v1 = vv[j][e];
+          p3d_adam1(w1, m1, v1, gg[j][e], alpha, omb1, omb2, eps);
+          ww[j][e] = w1; mm[j][e] = m1; vv[j][e] = v1; wn[e] = w1;
         }
-        if (!wsrc) *(f32x4*)(w + base) = ww[it];
-        *(f32x4*)(m + base) = mm[it]; *(f32x4*)(v + base) = vv[it];
+        if (!wsrc) *(f32x4*)(w + base) = ww[j];
+        *(f32x4*)(m + base) = mm[j]; *(f32x4*)(v + base) = vv[j];
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) tile[r][c + e] = wn[e];   // each thread rewrites only what it read
     }
+   }
   } else {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -1002,6 +1008,9 @@ struct WgradArgs {
   const float* alpha_dev;         // if set: the step's Adam alpha, formed by an earlier launch
 };
 
+#ifndef P3D_WG_PER_CU
+#define P3D_WG_PER_CU 5   // k_wgrad_multi workgroups per CU (round 5: 5 -- cfg3's 1,056 tiles in one round)
+#endif
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
 
 // Stage rows [mc, mc+64) x cols [c0, c0+64) of a packed or row-major [R, C] source, in two
@@ -1011,8 +1020,7 @@ struct WgradArgs {
 // round trips per staged chunk.)
 struct Stage64 { float f[16]; unsigned ok; };
 __device__ __forceinline__ void p3d_stage64_load(Stage64& st, const float* __restrict__ src, int pk, int64_t ld,
-                                                 int R, int C, int mc, int c0) {
-  const int tid = threadIdx.x;
+                                                 int R, int C, int mc, int c0, int tid = threadIdx.x) {
   st.ok = 0u;
   if (pk) {  // 16 packed 1 KB tiles (4 row tiles x 4 column groups); C is a multiple of 16
     const int ng = C >> 4;
@@ -1046,8 +1054,8 @@ __device__ __forceinline__ int p3d_wg_lidx(int r, int c) {
   return SW ? r * 64 + (c ^ ((r & 3) << 4)) : r * WG_LDS_STRIDE + c;
 }
 template <bool SW = false>
-__device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const Stage64& st, int pk) {
-  const int tid = threadIdx.x;
+__device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const Stage64& st, int pk,
+                                                  int tid = threadIdx.x) {
   if (pk) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1077,19 +1085,17 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
 #define P3D_WG_STAMP(k) do { } while (0)
 #endif
 // NOADAM: the gradient-only form (data-parallel steps, whose optimizer runs behind the
-// all-reduce): no optimizer code, swizzled 16 KB operand images and db's partials in the X image
-// once it is consumed -- 32 KB of LDS and 128 registers: 4 workgroups per CU, so 1,024 of cfg3's
-// 1,056 tiles run in the first round (the general form's 41 KB / 131 registers hold 3 per CU: 768 +
-// 288 tiles).  (The design aimed at 96 registers and 5 per CU -- one round -- but at that bound the
-// compiler spills 132 B per lane to scratch, tools/kdev.hip; measured per-CU occupancy is 4.)  The
-// same arithmetic: the same bits.
+// all-reduce): no optimizer code.  Both forms: swizzled 16 KB operand images, db's partials in LDS
+// the operands no longer need -- 32 KB of LDS -- and <= 96 registers (round 5: the staging addresses
+// formed inside the chunk loop, the fused Adam two rows of its four at a time, the layer picked with
+// constant indices), so five workgroups fit on a CU and all of cfg3's 1,056 tiles run in ONE round
+// (at four per CU: 1,024 + a 32-tile tail; at three, round 4: 768 + 288).  The same arithmetic:
+// the same bits.
 template <bool NOADAM = false>
 __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
   P3D_WG_STAMP(0);
-  // both forms use the swizzled 16 KB operand images (round 5: the fused form too -- 33 KB of
-  // LDS instead of 41 KB, so 4 workgroups fit on a CU and cfg3's 1,024 hidden-layer tiles run in
-  // one round instead of 768 + 256); one array, so the fused Adam's 64 x 65 transpose tile
-  // (16.6 KB) can run over into the dead dZ image
+  // both forms use the swizzled 16 KB operand images in one array, so the fused Adam's 64 x 65
+  // transpose tile (16.6 KB) can run over into the dead dZ image
   constexpr int XS = 64 * 64;
   __shared__ __attribute__((aligned(16))) float xz[2 * XS];
   float* xs = xz;
@@ -1100,18 +1106,24 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
   f32x4 acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __shared__ float dbp_own[NOADAM ? 1 : 4][64];
-  float (*dbp)[64] = NOADAM ? reinterpret_cast<float (*)[64]>(xs) : dbp_own;
+  // db's per-wave partials: in the X image once it is consumed (NOADAM), or past the part of the dZ
+  // image the Adam transpose tile runs over (fused form: 64 x 65 floats from xs) -- no LDS of
+  // their own, so the fused form fits five workgroups per CU (5 x 32 KB)
+  float (*dbp)[64] = NOADAM ? reinterpret_cast<float (*)[64]>(xs) : reinterpret_cast<float (*)[64]>(zs + 1024);
   const bool do_db = p.db && by == 0;
   float dbs = 0.f;   // wave w: rows 16w .. 16w+15 of column `lane` (summed in row order)
   // the step's alpha, requested before the contraction (its latency hides there)
   const float alpha_pre = (!NOADAM && p.adam && p.alpha_dev) ? *p.alpha_dev : 0.f;
   for (int mc = 0; mc < p.M; mc += 64) {
     Stage64 sx, sz;
-    p3d_stage64_load(sx, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0);
-    p3d_stage64_load(sz, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0);
-    p3d_stage64_store<true>(xs, sx, p.xpk);
-    p3d_stage64_store<true>(zs, sz, p.zpk);
+    // the staging addresses formed inside the chunk loop: hoisted out of it (a one-pass loop at
+    // B = 64) they stayed live across the whole tile and, at five workgroups per CU, in scratch
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    p3d_stage64_load(sx, p.X, p.xpk, p.ldx, p.M, p.K, mc, k0, tl);
+    p3d_stage64_load(sz, p.dZ, p.zpk, p.ldz, p.M, p.N, mc, n0, tl);
+    p3d_stage64_store<true>(xs, sx, p.xpk, tl);
+    p3d_stage64_store<true>(zs, sz, p.zpk, tl);
     __syncthreads();
     P3D_WG_STAMP(1);
 #pragma unroll NOADAM ? 2 : 4
@@ -1174,7 +1186,7 @@ __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int b
 #pragma unroll
       for (int r = 0; r < 4; ++r) tile[16 * w + 4 * q + r][16 * s + i] = acc[s][r];
     __syncthreads();
-    p3d_adam_tile64(tile, nullptr, p.woff, p.K, p.N, k0, n0, p.w, p.m, p.v, p.wd, p.wf, alpha,
+    p3d_adam_tile64<P3D_WG_PER_CU >= 5 ? 2 : 4>(tile, nullptr, p.woff, p.K, p.N, k0, n0, p.w, p.m, p.v, p.wd, p.wf, alpha,
                     1.0f - p.af.b1, 1.0f - p.af.b2, p.af.eps, p.af.wsrc);
 #ifdef P3D_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1240,6 +1252,29 @@ __device__ __forceinline__ void p3d_wgrad_multi_tile(const WgradMulti& mw, int b
     p3d_wgrad_tile<NOADAM>(p, loc % gx, loc / gx);
     return;
   }
+#if P3D_WG_PER_CU >= 5
+  // (the fused form at five per CU: the layer's fields picked with constant indices, as the
+  // gradient-only form does -- mw.ly[j] at a runtime j kept 29 registers' worth in scratch)
+#pragma unroll
+  for (int k = 1; k < P3D_WG_MULTI; ++k)
+    if (k < mw.n && b >= mw.begin[k]) j = k;
+#pragma unroll
+  for (int k = 0; k < P3D_WG_MULTI; ++k)
+    if (k == j) {
+      const WgradLayer& l = mw.ly[k];
+      p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
+      p.M = l.M; p.K = l.K; p.N = l.N; p.dW = l.dW; p.db = l.db;
+      p.woff = l.woff; p.boff = l.boff; p.wd = l.wd; p.wf = l.wf;
+      p.bn_adam = l.bn_adam; p.goff = l.goff; p.btoff = l.btoff;
+      beg = mw.begin[k]; gx = mw.gx[k];
+    }
+  if (mw.adam) {
+    p.adam = 1; p.af = mw.af; p.w = mw.w; p.m = mw.m; p.v = mw.v;
+    p.gflat = mw.gflat; p.alpha_dev = mw.alpha_dev;
+  }
+  const int loc = b - beg;
+  p3d_wgrad_tile<NOADAM>(p, loc % gx, loc / gx);
+#else
   while (j + 1 < mw.n && b >= mw.begin[j + 1]) ++j;
   const WgradLayer& l = mw.ly[j];
   p.X = l.X; p.ldx = l.ldx; p.xpk = l.xpk; p.dZ = l.dZ; p.ldz = l.ldz; p.zpk = l.zpk;
@@ -1252,6 +1287,7 @@ __device__ __forceinline__ void p3d_wgrad_multi_tile(const WgradMulti& mw, int b
   }
   const int loc = b - mw.begin[j];
   p3d_wgrad_tile<NOADAM>(p, loc % mw.gx[j], loc / mw.gx[j]);
+#endif
 }
 template <bool NOADAM>
 __device__ __forceinline__ void p3d_wgrad_multi_body(const WgradMulti& mw) {
@@ -1265,9 +1301,9 @@ __device__ __forceinline__ void p3d_wgrad_multi_body(const WgradMulti& mw) {
     st->global_step = st->global_step + 1;
   }
 }
-__global__ __launch_bounds__(256, 4) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
-// the gradient-only form, 4 workgroups (4 waves per SIMD) per CU (see p3d_wgrad_tile)
-__global__ __launch_bounds__(256, 4) void k_wgrad_grad(WgradMulti mw) { p3d_wgrad_multi_body<true>(mw); }
+__global__ __launch_bounds__(256, P3D_WG_PER_CU) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
+// the gradient-only form, P3D_WG_PER_CU workgroups per CU (see p3d_wgrad_tile)
+__global__ __launch_bounds__(256, P3D_WG_PER_CU) void k_wgrad_grad(WgradMulti mw) { p3d_wgrad_multi_body<true>(mw); }
 
 // A data-gradient launch carrying the weight-gradient (+ fused Adam) tiles of the layer above:
 // blocks [0, gx*gy) are k_dgrad's tiles of this layer, the rest mw's tiles (256 threads: the

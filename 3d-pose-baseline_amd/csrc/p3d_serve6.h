@@ -35,6 +35,15 @@
 #pragma once
 #include "p3d_serve.h"
 
+#ifndef P3D_S6_PIN_ARGS
+#define P3D_S6_PIN_ARGS 1          // the prologue's kernel arguments fetched in one round (round 5)
+#endif
+#ifndef P3D_S6_COMBINE_BATCH
+#define P3D_S6_COMBINE_BATCH 1     // the K-combine's LDS reads issued before the first add (round 5)
+#endif
+#ifndef P3D_S6_OUT_PRE
+#define P3D_S6_OUT_PRE 1           // the output layer's first weight fragments requested before the last hand-off
+#endif
 #ifndef P3D_S6_LATE_EPOCH
 #define P3D_S6_LATE_EPOCH 1        // the epoch read off the prologue's critical path (round 5)
 #endif
@@ -99,7 +108,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int OCH = RT * NCM < 4 ? RT * NCM : 4;   // output tiles per round of the output phase
   // activation ring depth (the wide forms cannot hold both rings DEPTH deep: 4 x 11 fragments
   // spilled 77 registers at NCM = 7, RT = 4)
+#ifndef P3D_S6_DA
   constexpr int DA = RT >= 6 ? (DEPTH >= 8 ? 4 : 2) : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);
+#else
+  constexpr int DA = RT >= 6 ? P3D_S6_DA : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);   // (development builds)
+#endif
 #ifndef P3D_S6_PD
   constexpr int PD = NCM <= 4 ? 2 : 1;       // ring slots prefetched off-contraction
 #else
@@ -118,6 +131,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // from LDS) go through readfirstlane: they end in scalar registers, and
   // buffer loads with a scalar offset need no per-lane waterfall loop
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+#if P3D_S6_PIN_ARGS
+  // (round 5) every argument the prologue reads, fetched from the kernel-argument segment at once:
+  // left to itself the compiler loaded them where they are used, several behind branches on earlier
+  // ones -- a chain of six dependent scalar-load round trips to a segment the host wrote just before
+  // the launch (cold in every cache), ~3 us before the first operand request
+  asm volatile("" ::"s"(p.split), "s"(p.delay), "s"(p.delay_xcc), "s"(p.census_extra), "s"(p.max_groups),
+               "s"(p.nb), "s"(p.L), "s"(p.K0), "s"(p.nblk), "s"(p.M), "s"(p.x), "s"(p.epoch), "s"(p.ecg),
+               "s"(p.err), "s"(p.sync), "s"(p.act), "s"(p.ly[0].Wf), "s"(gridDim.x));
+#endif
   const int L = p.L, ngL = L >> 4, T = ngL, ngK0 = p.K0 >> 4;
   const int q4 = 4 * (lane >> 4);
   const int S = min(max(p.split, 1), 8);   // (an out-of-range split is reported below, never divided by)
@@ -153,6 +175,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     sh[0] = (int)(((unsigned)xcc - blockIdx.x) & 7u);   // (trace: the launch's starting XCD)
     sh[2] = bad ? 1 : 0;
     sh[4] = 0;                               // some wave of this workgroup is broken (group_sync)
+    // no epoch word to advance until the first group_sync names one: a workgroup whose group takes
+    // no unit never reaches a group_sync, and its end reads this slot (P3D_S6_LATE_EPOCH; a first
+    // build left it unset and such a workgroup advanced a word at a stale LDS offset)
+    sh[5] = -1;
     if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
@@ -329,9 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // epilogue of tile t (chunk position cc) of layer l: z = acc / maxnorm + b, relu(z * inv + shift)
   // acc already divided by the max-norm divisor (maxnorm_div, a uniform branch of its own:
   // a per-element select made every epilogue run the division sequence)
-  auto epi_t = [&](int l, int cs, f32x4 acc) -> f32x4 {   // cs = tile - t_lo < ECT
-    const float* e = ec + (l * ECT + cs) * 48 + q4;
-    const f32x4 b4 = *(const f32x4*)e, inv4 = *(const f32x4*)(e + 16), sh4 = *(const f32x4*)(e + 32);
+  auto epi_c = [&](const f32x4& b4, const f32x4& inv4, const f32x4& sh4, f32x4 acc) -> f32x4 {
     f32x4 o;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -339,6 +363,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       o[k] = fmaxf(p.bn ? z * inv4[k] + sh4[k] : z, 0.0f);
     }
     return o;
+  };
+  auto epi_t = [&](int l, int cs, f32x4 acc) -> f32x4 {   // cs = tile - t_lo < ECT
+    const float* e = ec + (l * ECT + cs) * 48 + q4;
+    return epi_c(*(const f32x4*)e, *(const f32x4*)(e + 16), *(const f32x4*)(e + 32), acc);
   };
   auto maxnorm_div = [&](int l, f32x4& acc) {
     const float mx = ecm[l];
@@ -422,6 +450,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
 
   const float qnan = __builtin_nanf("");
+  // The output phase's first weight fragments (the member's first output tile, the first 2 OGH
+  // k-groups of this wave's K slice): they depend on nothing of the step, so the last hidden phase
+  // requests them after its epilogue stores, and their memory round trip runs under the hand-off
+  // (whose drain waits for them with the stores) instead of after it.  Requested whether or not the
+  // member has an output tile (a valid tile's address then): a fixed number of loads.
+  constexpr int OGH = 8;
+  f32x4 ow0[OGH], ow1[OGH];
+  auto out_wpre = [&]() {
+    const int oo = ((RT * NDT * r) / n) % NDT;
+    const __amdgpu_buffer_rsrc_t r4 = p3d_rsrc(lo.Wf);
+#pragma unroll
+    for (int g = 0; g < OGH; ++g) {
+      ow0[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r4, ((oo * ngL + gb + min(g, gcount - 1)) * 64 + lane) * 16, 0, 0));
+      ow1[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r4, ((oo * ngL + gb + min(OGH + g, gcount - 1)) * 64 + lane) * 16, 0, 0));
+    }
+  };
   // The output layer of the step at orow0 (round 5: its own phase instead of per-tile partials
   // summed by a reduction): the unit's RT x NDT output tiles are dealt contiguously over the
   // members; each tile is contracted over K = L as every hidden tile is -- wave w the k-groups of
@@ -445,13 +489,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // the K slice in halves of 8 k-groups, both halves' fragments requested before the first
         // MFMA (32 loads at L = 1024: the hidden rings are dead here; two 8-entry arrays stay in
         // registers where one 16-entry array went to scratch)
-        constexpr int GH = 8;
-        auto ld_half = [&](int gs, f32x4 (&av)[GH], f32x4 (&wv)[GH]) {
+        constexpr int GH = OGH;
+        auto ld_half = [&](int gs, f32x4 (&av)[GH], f32x4 (&wv)[GH], bool wpre) {
 #pragma unroll
           for (int g = 0; g < GH; ++g) {
             const int gg = gb + min(gs + g, gcount - 1);
             av[g] = p3d_ld_sc1(ry, ((ort * ngL + gg) * 64 + lane) * 16);
-            wv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r4, ((oo * ngL + gg) * 64 + lane) * 16, 0, 0));
+            if (!wpre)
+              wv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r4, ((oo * ngL + gg) * 64 + lane) * 16, 0, 0));
           }
         };
         auto mma_half = [&](int gs, const f32x4 (&av)[GH], const f32x4 (&wv)[GH]) {
@@ -464,8 +509,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         };
         for (int g0 = 0; g0 < gcount; g0 += 2 * GH) {
           f32x4 a0[GH], w0[GH], a1[GH], w1[GH];
-          ld_half(g0, a0, w0);
-          ld_half(g0 + GH, a1, w1);
+          // the member's first tile: its first 2 GH weight fragments came with the last hand-off
+          const bool wpre = P3D_S6_OUT_PRE && c0 == o_lo && j == 0 && g0 == 0;
+          if (wpre) {
+#pragma unroll
+            for (int g = 0; g < GH; ++g) { w0[g] = ow0[g]; w1[g] = ow1[g]; }
+          }
+          ld_half(g0, a0, w0, wpre);
+          ld_half(g0 + GH, a1, w1, wpre);
           mma_half(g0, a0, w0);
           mma_half(g0 + GH, a1, w1);
         }
@@ -474,9 +525,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int j = 0; j < OCH; ++j) red[(w * OCH + j) * 64 + lane] = oacc[j];
       __syncthreads();
       if (w < nt) {                            // wave j sums tile j's four slices in slice order
-        f32x4 tot = red[(0 * OCH + w) * 64 + lane];
+        f32x4 sl[4];                           // (all four requested before the first add)
 #pragma unroll
-        for (int k = 1; k < 4; ++k) tot += red[(k * OCH + w) * 64 + lane];
+        for (int k = 0; k < 4; ++k) sl[k] = red[(k * OCH + w) * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 tot = sl[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) tot += sl[k];
         if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
         p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
       }
@@ -618,6 +673,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __syncthreads();
         P3D_S6_STAMP(trs && first_c, 8 * ph + 2);
         f32x4 sacc[UMAX];                      // K slices summed in slice order, this wave's tiles
+#if P3D_S6_COMBINE_BATCH
+        {
+          // (round 5) every slice of every tile of the wave, and the tiles' epilogue constants,
+          // requested before the first add: left to itself the scheduler interleaved each read with
+          // the adds that consume it -- 15 dependent LDS round trips per phase (0.9 us in the trace)
+          f32x4 part[UMAX][4], ce[UMAX][3];
+#pragma unroll
+          for (int j = 0; j < UMAX; ++j) {
+            const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) part[j][k] = red[((k * RT + rt) * NCM + cc) * 64 + lane];
+            const int t = c0 + (cc < nck ? cc : nck - 1);
+            const float* e = ec + (ph * ECT + (t - t_lo)) * 48 + q4;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ce[j][k] = *(const f32x4*)(e + 16 * k);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < UMAX; ++j) {
+            sacc[j] = part[j][0];              // slice 0, tile (rt, cc), then 1, 2, 3
+#pragma unroll
+            for (int k = 1; k < 4; ++k) sacc[j] += part[j][k];
+          }
+          P3D_S6_STAMP(trs && first_c, 8 * ph + 5);
+          if (wsq_any)
+#pragma unroll
+            for (int j = 0; j < UMAX; ++j) maxnorm_div(ph, sacc[j]);
+#pragma unroll
+          for (int j = 0; j < UMAX; ++j) {
+            const int u = w + 4 * j, rt = u / NCM, cc = u % NCM;
+            if (u >= RT * NCM || cc >= nck) continue;
+            const int t = c0 + cc;
+            f32x4 yv = epi_c(ce[j][0], ce[j][1], ce[j][2], sacc[j]);
+            if (res) yv += rv[j];
+            *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
+          }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < UMAX; ++j) {
           const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
@@ -638,12 +731,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if (res) yv += rv[j];
           *(f32x4*)(Y + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
         }
+#endif
         P3D_S6_STAMP(trs && first_c, 8 * ph + 6);
         // red / rsum are rewritten by this member's next contraction of the phase
         if (c0 + NCM < t_hi) __syncthreads();
       }
       // the next step's input layer (it depends on nothing of this step) in the last phase
       if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, c0n, t_lo);
+      if (P3D_S6_OUT_PRE && lastp) out_wpre();
       P3D_S6_STAMP(trs, 8 * ph + 3);
       if (second) cur = t2;
       // every phase's hand-off: each wave waits for the members whose output its K slice reads
@@ -654,6 +749,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     out_phase(row0);                         // this step's output layer
 #ifdef P3D_TRACE
     if (trs && tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
+    if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[20480 + blockIdx.x] = wall_clock64();   // every member's end
 #endif
     trs = false;
     c0b = c0n;

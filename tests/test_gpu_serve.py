@@ -228,8 +228,8 @@ def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_
 @pytest.mark.parametrize("split,rt", [(1, 4), (2, 4), (3, 4), (5, 2), (1, 10)])
 def test_serve6_many_steps_per_group(monkeypatch, split, rt):
     """k_serve6 forced on a long launch (P3D_SERVE6=2): every group runs many steps, so the
-    next step's input layer rides in the last phase and each step's output is reduced in the
-    next step's first phase (split over the members); every row vs the oracle / k_serve5."""
+    next step's input layer rides in the last phase and each step's output layer runs as its own
+    phase after that hand-off (tiles dealt over the members); every row vs the oracle / k_serve5."""
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     B = 64 * 300 + 9
     x = np.random.default_rng(77 + split).standard_normal((B, 32)).astype(np.float32)

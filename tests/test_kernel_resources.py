@@ -76,3 +76,13 @@ def test_no_kernel_uses_dynamic_stack(res):
     runtime default, not something the metadata bounds)."""
     bad = [k for k, r in res.items() if r.get("uses_dynamic_stack")]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["k_wgrad_multi", "k_wgrad_grad"])
+def test_weight_gradient_kernels_fit_five_per_cu(res, name):
+    """cfg3's 1,056 weight-gradient tiles run in ONE round only at five 256-thread workgroups per CU
+    (1,280 slots): <= 32 KB of LDS (5 x 32 KB = the CU's 160 KB) and <= 96 registers (VGPR + AGPR,
+    allocated in 8s: 5 waves per SIMD).  A change that grows either brings back the 32-tile tail."""
+    r = _find(res, name)
+    assert r.get("group_segment_fixed_size", 0) <= 32768, (name, r)
+    assert r.get("vgpr_count", 0) + r.get("agpr_count", 0) <= 96, (name, r)

@@ -25,6 +25,9 @@ def main():
             res = json.loads(line[-1]) if (p.returncode == 0 and line) else {"rc": p.returncode, "err": p.stderr[-500:]}
             out["runs"].append({"round": r, "env": tag, **res})
             print(json.dumps(out["runs"][-1]), flush=True)
+            if "rc" in res:   # a failed run (a GPU fault among the causes): run nothing more on the GPU
+                print(json.dumps(out))
+                sys.exit(2)
     print(json.dumps(out))
 
 

@@ -76,6 +76,13 @@ def main():
                           "per_xcd_last_start": [round(float(((wg[(wg[:, 3] & 255) == x, 0] - t0) / 100.0).max()), 2)
                                                  if ((wg[:, 3] & 255) == x).any() else None for x in range(8)],
                           "start_xcd_offsets": sorted(set(int(v) for v in ((wg[:, 3] >> 16) & 255)))}))
+    # every workgroup's end (round 5 builds: after the output phase)
+    ends = buf[20480:20480 + 1024].astype(np.int64)
+    ends = ends[ends >= t0]
+    if len(ends):
+        e = np.sort((ends - t0) / 100.0)
+        print(json.dumps({"workgroup_end_q": [round(float(np.quantile(e, f)), 2) for f in (0, 0.25, 0.5, 0.75, 0.9, 1.0)],
+                          "launch_end_us": round(float(e[-1]), 2)}))
 
 
 if __name__ == "__main__":
