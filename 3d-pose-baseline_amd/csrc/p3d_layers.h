@@ -1009,7 +1009,11 @@ struct WgradArgs {
 };
 
 #ifndef P3D_WG_PER_CU
-#define P3D_WG_PER_CU 5   // k_wgrad_multi workgroups per CU (round 5: 5 -- cfg3's 1,056 tiles in one round)
+// k_wgrad_multi / k_wgrad_grad workgroups per CU.  5 fits (32 KB LDS, <= 96 registers: cfg3's 1,056
+// tiles in one round instead of 1,024 + a 32-tile tail) but measured SLOWER on the box: 28.6-28.9 vs
+// 25.6-26.0 us per launch (r05_t8, three alternating pairs) -- five tiles' requests per CU contend
+// more than the tail costs; 4 stays the default, 5 is a build option
+#define P3D_WG_PER_CU 4
 #endif
 #define WG_LDS_STRIDE 80   // 64 + 16 pad: lanes q and q+1 (adjacent rows) hit disjoint banks
 
@@ -1086,11 +1090,11 @@ __device__ __forceinline__ void p3d_stage64_store(float* __restrict__ dst, const
 #endif
 // NOADAM: the gradient-only form (data-parallel steps, whose optimizer runs behind the
 // all-reduce): no optimizer code.  Both forms: swizzled 16 KB operand images, db's partials in LDS
-// the operands no longer need -- 32 KB of LDS -- and <= 96 registers (round 5: the staging addresses
-// formed inside the chunk loop, the fused Adam two rows of its four at a time, the layer picked with
-// constant indices), so five workgroups fit on a CU and all of cfg3's 1,056 tiles run in ONE round
-// (at four per CU: 1,024 + a 32-tile tail; at three, round 4: 768 + 288).  The same arithmetic:
-// the same bits.
+// the operands no longer need -- 32 KB of LDS -- and the staging addresses formed inside the chunk
+// loop: 4 workgroups per CU (1,024 of cfg3's 1,056 tiles in the first round; round 4's 41 KB form
+// held 3: 768 + 288).  With P3D_WG_PER_CU = 5 the fused Adam runs two rows of its four at a time and
+// the layer is picked with constant indices: <= 96 registers, five per CU, one round -- measured
+// slower (P3D_WG_PER_CU above).  The same arithmetic: the same bits.
 template <bool NOADAM = false>
 __device__ __forceinline__ void p3d_wgrad_tile(const WgradArgs& p, int bx, int by) {
   P3D_WG_STAMP(0);

@@ -209,30 +209,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // first-unit input-layer operands (this wave's tiles) and the epilogue-constant table rows
   f32x4 xa0[UMAX][4], wb0[UMAX][4];
   float vec[ECN], wq = 1.f;
+  // Every request unconditional, from a clamped (always valid) address, the unused ones discarded
+  // (round 5): behind per-request guards each request sat in a block of its own, and at this
+  // kernel's scalar-register pressure the compiler re-fetched the argument words it needed (x, W0,
+  // the table) from the argument segment in every block, each with a wait -- ~30 dependent scalar
+  // round trips before the last operand request (the trace's 2.7 us from start to placement).
   auto prefetch = [&](int gi_, int tlo, int thi) {
-    if (gi_ >= 0 && gi_ < p.nb && tlo < thi) {
-      const int nck = min(NCM, thi - tlo);
+    const int nck = max(min(NCM, thi - tlo), 1);
 #pragma unroll
-      for (int j = 0; j < UMAX; ++j) {
-        const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
-        int64_t rowc = (int64_t)gi_ * ROWS + 16 * rt + (lane & 15);
-        rowc = rowc < p.M ? rowc : p.M - 1;
-        const int t = tlo + (cc < nck ? cc : nck - 1);
+    for (int j = 0; j < UMAX; ++j) {
+      const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+      int64_t rowc = (int64_t)gi_ * ROWS + 16 * rt + (lane & 15);
+      rowc = rowc < p.M ? (rowc > 0 ? rowc : 0) : p.M - 1;
+      const int t = min(max(tlo + (cc < nck ? cc : nck - 1), 0), T - 1);
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          if (g < ngK0) {
-            xa0[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
-            wb0[j][g] = *(const f32x4*)(p.ly[0].Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
-          }
+      for (int g = 0; g < 2; ++g) {          // K0 <= 32 (the reference's 16 joints x 2): all of it
+        const int gg = min(g, ngK0 - 1);   // (g >= ngK0: a copy of the last k-group, never used)
+        xa0[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * gg + q4);
+        wb0[j][g] = *(const f32x4*)(p.ly[0].Wf + ((int64_t)(t * ngK0 + gg) * 64 + lane) * 4);
+      }
+      if (ngK0 > 2) {                        // (one uniform branch for K0 in (32, 64])
+#pragma unroll
+        for (int g = 2; g < 4; ++g) {
+          const int gg = min(g, ngK0 - 1);
+          xa0[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * gg + q4);
+          wb0[j][g] = *(const f32x4*)(p.ly[0].Wf + ((int64_t)(t * ngK0 + gg) * 64 + lane) * 4);
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < ECN; ++k) {
-      const int idx = tid + 256 * k;
-      const int l = idx / (ECT * 48), rem = idx % (ECT * 48), cs = rem / 48, j = rem % 48;
-      vec[k] = idx < tot_ec ? p.ecg[((int64_t)l * T + min(tlo + cs, T - 1)) * 48 + j] : 0.f;
+      const int idx = tid + 256 * k, idc = idx < tot_ec ? idx : 0;
+      const int l = idc / (ECT * 48), rem = idc % (ECT * 48), cs = rem / 48, j = rem % 48;
+      const float e = p.ecg[((int64_t)l * T + min(tlo + cs, T - 1)) * 48 + j];
+      vec[k] = idx < tot_ec ? e : 0.f;
     }
-    wq = tid < nl_ec ? p.ecg[(int64_t)nl_ec * T * 48 + tid] : 1.f;
+    const float e = p.ecg[(int64_t)nl_ec * T * 48 + (tid < nl_ec ? tid : 0)];
+    wq = tid < nl_ec ? e : 1.f;
   };
   // (unconditional: placement under a guard made the compiler keep its results in a form that cost
   // the main loop 52 AGPRs of its allocation and ~20 us per launch; gid is only used to address
@@ -335,11 +348,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       rowc = rowc < p.M ? rowc : p.M - 1;
       const int t = c0 + (cc < nck ? cc : nck - 1);
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        if (g < ngK0) {
-          xa[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * g + q4);
-          wb[j][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + g) * 64 + lane) * 4);
+      for (int g = 0; g < 2; ++g) {          // (as in prefetch)
+        const int gg = min(g, ngK0 - 1);
+        xa[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * gg + q4);
+        wb[j][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + gg) * 64 + lane) * 4);
+      }
+      if (ngK0 > 2) {
+#pragma unroll
+        for (int g = 2; g < 4; ++g) {
+          const int gg = min(g, ngK0 - 1);
+          xa[j][g] = *(const f32x4*)(p.x + rowc * p.K0 + 16 * gg + q4);
+          wb[j][g] = *(const f32x4*)(li.Wf + ((int64_t)(t * ngK0 + gg) * 64 + lane) * 4);
         }
+      }
     }
   };
   {   // epilogue constants of this member's tiles -- bias, inv = gamma / sqrt(var + eps),
