@@ -115,7 +115,7 @@ struct p3d_model {
   int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
   int xchg_wk = 8;            // BN-train hidden exchange-form forward: 8 waves with an 8-deep ring (measured and
                               // pruned in round 4: 16 waves 8.6 vs 6.8 us; rings of 4 / 2 within 1 %)
-  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8)
+  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8, 4)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -615,6 +615,11 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_ATTACH")) m->wgrad_attach = atoi(ev);
+  // the attached form's launches hold a data-gradient tile and the layer above's weight-gradient
+  // tiles side by side on a CU: 256-thread workgroups (the data-gradient K split over 4 waves, in
+  // every hidden dgrad of the model so both forms keep giving the same bits); a 16-wave workgroup
+  // fills its CU and the weight-gradient tiles would queue behind it
+  if (m->wgrad_attach && !getenv("P3D_DGRAD_WK")) m->dgrad_wk = 4;
   if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_WGRAD_SIDE")) m->wgrad_side = atoi(ev);
   if (m->wgrad_side) {   // created here, never while a caller captures a graph
@@ -1894,14 +1899,20 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
         ProfScope ps(m, is_out ? "dgrad_out" : carry ? "dgrad_wgrad" : "dgrad_hidden");
         if (carry) {
           const int gx = (int)grid.x, gy = (int)grid.y;
-          go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, dim3((unsigned)(gx * gy + mw.begin[mw.n])), dim3(512), st, a, mw,
-             gx, gy);
+          // (round 5) the data-gradient tiles in the same 16-wave split and sibling remap as the
+          // plain launch (the same bits either way; the remap keeps the exchange XCD-local)
+          if (xchg && m->xchg_remap && gx % 8 == 0) a.remap_gy = gy;
+          const dim3 gw((unsigned)(gx * gy + mw.begin[mw.n]));
+          if (m->dgrad_wk == 4) go(ps, k_dgrad_wg<1, 4, 4, 2, true, 1>, gw, dim3(256), st, a, mw, gx, gy);
+          else if (m->dgrad_wk == 16) go(ps, k_dgrad_wg<1, 16, 4, 2, true, 1>, gw, dim3(1024), st, a, mw, gx, gy);
+          else go(ps, k_dgrad_wg<1, 8, 8, 2, true, 1>, gw, dim3(512), st, a, mw, gx, gy);
         } else if (dz_pk) {
           dim3 g = grid;
           if (xchg && m->xchg_remap && grid.x % 8 == 0) { a.remap_gy = (int)grid.y; g = dim3(grid.x * grid.y); }
           // 16 waves (both BN forms, so they keep giving the same bits): 6.8 vs 7.0-7.1 us per
-          // hidden dgrad (A/B, one box); the attached-wgrad form keeps k_dgrad_wg's 8-wave split
-          if (m->dgrad_wk == 16 && !m->wgrad_attach) go(ps, k_dgrad<1, 16, 4, 2, true, 1>, g, dim3(1024), st, a);
+          // hidden dgrad (A/B, one box); the attached form uses the same split
+          if (m->dgrad_wk == 16) go(ps, k_dgrad<1, 16, 4, 2, true, 1>, g, dim3(1024), st, a);
+          else if (m->dgrad_wk == 4) go(ps, k_dgrad<1, 4, 4, 2, true, 1>, g, dim3(256), st, a);
           else go(ps, k_dgrad<1, 8, 8, 2, true, 1>, g, dim3(512), st, a);
         } else {
           dim3 g = grid;

@@ -1319,6 +1319,12 @@ template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
 __global__ __launch_bounds__(64 * WK) void k_dgrad_wg(BwdArgs p, WgradMulti mw, int gx, int gy) {
   const int b = blockIdx.x, nd = gx * gy;
   if (b < nd) {
+    if (p.remap_gy > 0) {   // (the exchange siblings of a column tile on one XCD, as k_dgrad)
+      int bx, by;
+      p3d_sibling_remap(b, gx, gy, bx, by);
+      p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, bx, by, gy);
+      return;
+    }
     p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, b % gx, b / gx, gy);
     return;
   }
