@@ -444,21 +444,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // input layer (K0 = input_size <= 64) of the member's tiles for the rows of the step at
   // rbase, row tile w, into act buffer cbuf: the rows loaded once, then every tile's weight
   // fragments requested before the first MFMA (one round of load latency, not one per tile)
+  // (round 5: the wave's tiles contracted side by side -- one block per k-group, the tiles' MFMA
+  // chains interleaved instead of one tile's 8 dependent MFMAs after another's -- and their epilogue
+  // constants requested before the first MFMA; every tile's sum in the same order: the same bits)
   auto in_compute = [&](int c0, const f32x4 (&xa)[UMAX][4], const f32x4 (&wb)[UMAX][4], int cbuf) {
     const int nck = min(NCM, t_hi - c0);
+    f32x4 acc[UMAX], ce[UMAX][3];
+#pragma unroll
+    for (int j = 0; j < UMAX; ++j) {
+      acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int u = min(w + 4 * j, RT * NCM - 1), cc = u % NCM;
+      const int t = c0 + (cc < nck ? cc : nck - 1);
+      const float* e = ec + (0 * ECT + (t - t_lo)) * 48 + q4;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ce[j][k] = *(const f32x4*)(e + 16 * k);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g < ngK0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < UMAX; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[j][g][e], xa[j][g][e], acc[j], 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < UMAX; ++j) {
       const int u = w + 4 * j, rt = u / NCM, cc = u % NCM;
       if (u >= RT * NCM || cc >= nck) continue;
       const int t = c0 + cc;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        if (g < ngK0)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[j][g][e], xa[j][g][e], acc, 0, 0, 0);
-      if (wsq_any) maxnorm_div(0, acc);
-      const f32x4 y = epi_t(0, t - t_lo, acc);
+      if (wsq_any) maxnorm_div(0, acc[j]);
+      const f32x4 y = epi_c(ce[j][0], ce[j][1], ce[j][2], acc[j]);
       *(f32x4*)(act + cbuf * slab + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = y;
     }
   };
@@ -494,9 +508,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the W4 fragment), then the four slices summed in slice order -- so the association is fixed by
   // the tile and every launch form gives the same bits.  Reads slab 3 after the last phase's
   // hand-off (this wave's K-slice producers); nothing is written but y.
+#ifdef P3D_TRACE   // output-phase detail, every workgroup (tools/trace_serve6.py): 21504 + 4 b + k
+#define P3D_S6_OSTAMP(k)                                                                               \
+  do {                                                                                                 \
+    if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[21504 + blockIdx.x * 4 + (k)] = wall_clock64();     \
+  } while (0)
+#else
+#define P3D_S6_OSTAMP(k) do { } while (0)
+#endif
   auto out_phase = [&](int64_t orow0) {
     constexpr int OT = RT * NDT;
     const int o_lo = (OT * r) / n, o_hi = (OT * (r + 1)) / n;
+    P3D_S6_OSTAMP(0);
     const __amdgpu_buffer_rsrc_t ry = p3d_rsrc(act + 3 * slab), r4 = p3d_rsrc(lo.Wf);
     for (int c0 = o_lo; c0 < o_hi; c0 += OCH) {
       const int nt = min(OCH, o_hi - c0);
@@ -544,6 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
 #pragma unroll
       for (int j = 0; j < OCH; ++j) red[(w * OCH + j) * 64 + lane] = oacc[j];
+      if (c0 == o_lo) P3D_S6_OSTAMP(1);
       __syncthreads();
       if (w < nt) {                            // wave j sums tile j's four slices in slice order
         f32x4 sl[4];                           // (all four requested before the first add)
@@ -556,6 +580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
         p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
       }
+      if (c0 == o_lo) P3D_S6_OSTAMP(2);
       __syncthreads();                         // red is rewritten next (next round / phase)
     }
   };
@@ -626,6 +651,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int cc = 0; cc < NCM; ++cc) rb_[d][cc] = d < PD ? rbp[d < PD ? d : 0][cc] : ldb(cc, d);
         }
+#ifdef P3D_TRACE   // (trace builds: the ring's first operands in hand -- the phase-start bubble)
+        if (trs && first_c) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          P3D_S6_STAMP(true, 8 * ph + 7);
+        }
+#endif
         f32x4 acc[NCM][RT];
 #pragma unroll
         for (int cc = 0; cc < NCM; ++cc)
@@ -760,6 +791,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // the next step's input layer (it depends on nothing of this step) in the last phase
       if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, c0n, t_lo);
       if (P3D_S6_OUT_PRE && lastp) out_wpre();
+      if (lastp) P3D_S6_OSTAMP(3);
       P3D_S6_STAMP(trs, 8 * ph + 3);
       if (second) cur = t2;
       // every phase's hand-off: each wave waits for the members whose output its K slice reads

@@ -58,7 +58,9 @@ def main():
         wall = sum(row[8 * p + 1] - row[8 * p] for p in range(1, NH + 1))
         out.append({"group": g, "row": r, "clock_ghz": round(cyc / max(wall, 1) / 10.0, 3), "start": us(row[0]), "census": us(row[1]), "input": us(row[2]),
                     "consts": us(row[4]), "in_mfma": us(row[5]), "handoff0": us(row[3]), "end_phase": [us(row[8 * p + 4]) for p in range(1, NH + 1)],
-                    "reduce_end": us(row[8 * (NH + 1)]), "phases_us": ph})
+                    "reduce_end": us(row[8 * (NH + 1)]), "phases_us": ph,
+                    # (trace builds: phase start to the ring's first operands in hand)
+                    "ring_fill_us": [round((row[8 * p + 7] - row[8 * p]) / 100, 2) for p in range(1, NH + 1)]})
     out.sort(key=lambda d: d["reduce_end"])
     for d in out:
         print(json.dumps(d))
@@ -76,6 +78,18 @@ def main():
                           "per_xcd_last_start": [round(float(((wg[(wg[:, 3] & 255) == x, 0] - t0) / 100.0).max()), 2)
                                                  if ((wg[:, 3] & 255) == x).any() else None for x in range(8)],
                           "start_xcd_offsets": sorted(set(int(v) for v in ((wg[:, 3] >> 16) & 255)))}))
+    # output phase per workgroup (round 5): 3 last phase's stores issued, 0 its hand-off done,
+    # 1 first tile contracted, 2 first tile stored
+    o = buf[21504:21504 + 256 * 4].astype(np.int64).reshape(256, 4)
+    ok = (o[:, 0] >= t0) & (o[:, 3] >= t0)
+    if ok.any():
+        o = o[ok]
+        qq = lambda a: [round(float(np.quantile(a, f)), 2) for f in (0, 0.1, 0.5, 0.9, 1.0)]   # noqa: E731
+        has = o[:, 2] > o[:, 0]   # workgroups with an output tile
+        print(json.dumps({"out_last_handoff_us_q": qq((o[:, 0] - o[:, 3]) / 100.0),
+                          "out_contract_us_q": qq((o[has, 1] - o[has, 0]) / 100.0) if has.any() else None,
+                          "out_store_us_q": qq((o[has, 2] - o[has, 1]) / 100.0) if has.any() else None,
+                          "out_entry_q": qq((o[:, 0] - t0) / 100.0), "tiles": int(has.sum())}))
     # every workgroup's end (round 5 builds: after the output phase)
     ends = buf[20480:20480 + 1024].astype(np.int64)
     ends = ends[ends >= t0]
