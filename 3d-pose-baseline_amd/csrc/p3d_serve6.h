@@ -566,7 +566,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
 #pragma unroll
-      for (int j = 0; j < OCH; ++j) red[(w * OCH + j) * 64 + lane] = oacc[j];
+      for (int j = 0; j < OCH; ++j)
+        if (j < nt) red[(w * OCH + j) * 64 + lane] = oacc[j];   // (only the round's live tiles)
       if (c0 == o_lo) P3D_S6_OSTAMP(1);
       __syncthreads();
       if (w < nt) {                            // wave j sums tile j's four slices in slice order
