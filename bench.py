@@ -51,15 +51,31 @@ def flops_per_pose(L=L, N=NBLK):
     return 2 * (IN * L + 2 * N * L * L + OUT * L)
 
 
+def _free_port():
+    """A free 127.0.0.1 port below the kernel's ephemeral range (32768-60999): a port the OS handed
+    out and we released can go to another socket (RCCL / gloo open many) before the rendezvous binds
+    it -- the EADDRINUSE flake seen once in the GPU tests (r05_t20)."""
+    import random
+    import socket
+    for _ in range(64):
+        p = random.randint(20000, 29999)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def launch_ranks(n, dry=False):
     """`bench.py --gpus N` outside a launcher: run N ranks of this script under
     torch.distributed.run (127.0.0.1 rendezvous, a free port) as a child process and
     return its exit code.  Rank 0 prints the JSON line."""
-    import socket
     import subprocess
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = _free_port()
     argv = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
@@ -93,14 +109,11 @@ def setup_dist():
 def init_world1_group():
     """A 1-rank RCCL process group (127.0.0.1 rendezvous) so the data-parallel train step --
     bucketed all-reduce included -- can be timed on one GPU beside the fused single-GPU step."""
-    import socket
     import torch
     import torch.distributed as dist
     if dist.is_initialized():
         return False
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = _free_port()
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
                             device_id=torch.device("cuda", torch.cuda.current_device()))
     return True

@@ -20,6 +20,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port():
+    # a port below the kernel's ephemeral range (32768-60999): a port the OS handed out and we
+    # released can be handed to another socket (RCCL / gloo open many) before the rendezvous binds
+    # it -- the EADDRINUSE flake of r05_t20.  A random pick in 20000-29999, checked free.
+    import random
+    for _ in range(64):
+        p = random.randint(20000, 29999)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        return p
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
