@@ -244,6 +244,7 @@ struct p3d_model {
   int serve6_split = 0;     // k_serve6 groups per XCD, 0 = chosen per launch (env P3D_SERVE6_SPLIT: 1..8)
   int serve6_rt = 0;        // k_serve6 row tiles per unit, 0 = chosen per launch (env P3D_SERVE6_RT: 4 or 2)
   int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
+  int serve6_pair = 0;      // XCD-wide units of 10 row tiles as two 5-row-tile units run side by side (env P3D_SERVE6_PAIR)
   std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
   // data-parallel step with the library's own all-reduce (p3d_dp.h)
   p3d_comm* comm = nullptr;      // not owned (p3d_comm_create / p3d_comm_destroy)
@@ -641,6 +642,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_SERVE6_SPLIT")) m->serve6_split = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_RT")) m->serve6_rt = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_DEPTH")) m->serve6_depth = atoi(ev);
+  if (const char* ev = getenv("P3D_SERVE6_PAIR")) m->serve6_pair = atoi(ev);
   {
     StepState s0{};
     s0.global_step = 0; s0.beta1_power = 0.9f; s0.beta2_power = 0.999f; s0.arrivals = 0;
@@ -1389,7 +1391,7 @@ static void launch_serve_k(const ProfScope& ps, const p3d_model* m, unsigned gri
 // A k_serve6 launch shape: S groups per XCD, RT row tiles per unit (4: batch-64 steps, 2:
 // 32-row half steps), NCM column tiles per contraction (the built form covering a member of the
 // smallest group; its epilogue constants of at most ECT tiles sit in LDS, p3d_serve6.h).
-struct Serve6Plan { int S = 0, rt = 4, ncm = 0; };
+struct Serve6Plan { int S = 0, rt = 4, ncm = 0; bool pair = false; };
 
 // the built (RT, NCM) forms: batch-64 units with 2 / 4 / 7 / 8 column tiles per CU, half-step
 // units with 11 (S = 5) or 2 (S = 1), 16-row units with 2 (S = 1: a lone batch-64 request on
@@ -1436,8 +1438,12 @@ static Serve6Plan serve6_plan(const p3d_model* m, int64_t B, int T) {
   return best;
 }
 
-static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, int rt, unsigned grid,
-                          hipStream_t st, const ServeArgs& a) {
+static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int depth, int rt, bool pair,
+                          unsigned grid, hipStream_t st, const ServeArgs& a) {
+  if (pair) {   // (serve6 PAIR: two units of rt row tiles per group)
+    go(ps, k_serve6<4, 3, 2, 5, true>, dim3(grid), dim3(256), st, a);
+    return;
+  }
   switch (rt) {   // half-step units (11 column tiles, S = 5) / XCD-wide units (2 tiles, S = 1)
     case 1: go(ps, k_serve6<4, 3, 2, 1>, dim3(grid), dim3(256), st, a); return;
     case 2:
@@ -1538,6 +1544,11 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     use6 = plan.S > 0;                       // no form covers this width: k_serve5
     // k_serve6's four activation slabs per group (8 S groups of 16 RT rows) in serve6_act
     if (use6 && (int64_t)8 * plan.S * 16 * plan.rt > P3D_SERVE6_ROWS) use6 = false;
+    // the pair form: an XCD-wide unit of 10 row tiles run as two units of 5 side by side
+    if (use6 && m->serve6_pair && plan.S == 1 && plan.rt == 10 && L / 64 >= 12) {
+      plan.rt = 5;
+      plan.pair = true;
+    }
     if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
   }
   a.ecg = m->serve_ecg;
@@ -1578,9 +1589,9 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     if (plan.rt == 1) depth = 4;
     if (plan.rt > 4) depth = 4;   // (an 8-deep weight ring measured 117 vs 107-112 us at RT = 10)
     m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ", " +
-                     std::to_string(plan.rt) + ">";
+                     std::to_string(plan.rt) + (plan.pair ? ", true>" : ">");
     ProfScope ps(m, "serve");
-    launch_serve6(ps, m, ncm, depth, plan.rt, (unsigned)m->serve_grid, st, a);
+    launch_serve6(ps, m, ncm, depth, plan.rt, plan.pair, (unsigned)m->serve_grid, st, a);
   } else {
     m->serve_kname.clear();
     ProfScope ps(m, "serve");

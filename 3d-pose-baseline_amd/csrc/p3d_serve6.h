@@ -100,9 +100,22 @@ __device__ __forceinline__ int p3d_tile_owner(int t, int n, int T) { return ((t 
 // CU per XCD and serves 10 row tiles (p3d.hip serve6_plan picks the form per launch).
 // The epilogue / input-layer work of a chunk, RT x NCM 16 x 16 tiles, is dealt to the waves
 // round-robin: unit u = w + 4 j is row tile u / NCM of column tile u % NCM (UMAX per wave).
-template <int DEPTH, int NDT, int NCM, int RT = 4>
+//
+// PAIR (round 5): each group runs TWO units of RT row tiles side by side, alternating their
+// phases -- A's phase ph, B's phase ph, A's phase ph + 1, ... -- so the hand-off of one unit runs
+// under the other's contraction instead of in front of the next: a member's next contraction
+// reads the other unit's previous phase, published a whole contraction earlier.  Per block
+// (one unit's phase): the contraction, whose last DEPTH k-groups refill the register ring with
+// the next block's first ones (its producers' flags checked a round earlier); partial sums to
+// LDS; K-combine, epilogue, stores; the next contraction at once, its ring full.  A block's
+// stores are published from inside the next contraction, after its first DEPTH k-groups (a
+// vmcnt wait that leaves that contraction's refills in flight), each wave on its own, the fourth
+// to arrive (an LDS counter) posting the member's flag -- no barrier, no store round trip and no
+// ring fill between contractions.
+template <int DEPTH, int NDT, int NCM, int RT = 4, bool PAIR = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_serve6(ServeArgs p) {
   static_assert(RT >= 1 && RT <= 16, "row tiles per unit");
+  static_assert(!PAIR || (NCM == 2 && DEPTH == 4), "the pair form: 2 column tiles per member, a 4-deep ring");
   constexpr int ROWS = 16 * RT;              // rows of one unit
   constexpr int UMAX = (RT * NCM + 3) / 4;   // 16 x 16 tiles a wave finishes per chunk
   constexpr int OCH = RT * NCM < 4 ? RT * NCM : 4;   // output tiles per round of the output phase
@@ -118,7 +131,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #else
   constexpr int PD = P3D_S6_PD;
 #endif
-  __shared__ __attribute__((aligned(16))) f32x4 red[4 * RT * NCM * 64];  // [slice][rt][tile][lane]
+  static_assert(!PAIR || DA == DEPTH, "the pair form's ring runs on across blocks: every slot holds both operands");
+  // [slice][rt][tile][lane] (PAIR: two of them, alternate blocks)
+  __shared__ __attribute__((aligned(16))) f32x4 red[(PAIR ? 2 : 1) * 4 * RT * NCM * 64];
   // epilogue constants of the member's tiles (up to ECT of them), per layer 0..2N:
   // bias | inv | shift, and each layer's max-norm divisor.  Every epilogue reads them from
   // LDS: no global load on a branch of the epilogue, so the compiler's vmcnt waits there stay
@@ -179,6 +194,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // no unit never reaches a group_sync, and its end reads this slot (P3D_S6_LATE_EPOCH; a first
     // build left it unset and such a workgroup advanced a word at a stale LDS offset)
     sh[5] = -1;
+    sh[6] = 0;                               // PAIR: waves past their store drain (publish counter)
     if (bad) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int nl_ec = 2 * p.nblk + 1, tot_ec = nl_ec * ECT * 48;
@@ -205,6 +221,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (gi >= ng) gi = p.nb;
     }
     if ((T + n - 1) / n > ECT) gi = -1;      // a placement the host did not size this form for
+    // (PAIR: one contraction of 1..NCM tiles per member, and two ring rounds before the last DEPTH
+    // k-groups -- a block posts the previous one after the first, checks the next one's producers
+    // before the last)
+    if (PAIR && ((T + n - 1) / n > NCM || n > T || (T >> 2) < 3 * DEPTH)) gi = -1;
   };
   // first-unit input-layer operands (this wave's tiles) and the epilogue-constant table rows
   f32x4 xa0[UMAX][4], wb0[UMAX][4];
@@ -216,8 +236,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // round trips before the last operand request (the trace's 2.7 us from start to placement).
   auto prefetch = [&](int gi_, int tlo, int thi) {
     const int nck = max(min(NCM, thi - tlo), 1);
+    // (PAIR: the input operands are requested by its prologue -- held from here they crowded the
+    // registers, and the compiler spilled each fragment as it arrived, a serial wait per load)
 #pragma unroll
-    for (int j = 0; j < UMAX; ++j) {
+    for (int j = 0; j < (PAIR ? 0 : UMAX); ++j) {
       const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
       int64_t rowc = (int64_t)gi_ * ROWS + 16 * rt + (lane & 15);
       rowc = rowc < p.M ? (rowc > 0 ? rowc : 0) : p.M - 1;
@@ -318,7 +340,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // slabs 0..2: the hidden layers' rotation; slab 3: the last hidden layer's output, the output
   // layer's input (the next step's input layer writes the slab of the rotation the last phase reads
   // nothing from, so the last phase's output needs a fourth)
-  float* act = p.act + (int64_t)gid * 4 * slab;
+  // (PAIR: unit B's four slabs follow unit A's)
+  float* act = p.act + (int64_t)gid * (PAIR ? 8 : 4) * slab;
   const ServeLayer& li = p.ly[0];
   const ServeLayer& lo = p.ly[2 * p.nblk + 1];
   const bool wsq_any = li.wsq != nullptr;
@@ -400,7 +423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // A member whose wait ran out is `broken`: it publishes its phases with the poison bit, every
   // member that reads a poisoned flag becomes broken too, and broken members store NaN instead
   // of their output elements -- rows of a unit whose hand-offs failed never carry wrong values.
-  auto group_sync = [&](bool full) {
+  auto group_sync = [&](bool full, bool wait = true) {   // (PAIR: posts without the wait too)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (broken) sh[4] = 1;
 #if P3D_S6_LATE_EPOCH
@@ -423,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       __hip_atomic_store(flags + r, nsync | (broken ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int m0 = full ? 0 : p3d_tile_owner(gb, n, T);
     const int cnt = full ? n : p3d_tile_owner(gb + gcount - 1, n, T) - m0 + 1;
-    if (!broken) {
+    if (wait && !broken) {
       int spin = 0;
       while (true) {
         const unsigned v = lane < cnt ? __hip_atomic_load(flags + m0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -447,7 +470,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (round 5: the wave's tiles contracted side by side -- one block per k-group, the tiles' MFMA
   // chains interleaved instead of one tile's 8 dependent MFMAs after another's -- and their epilogue
   // constants requested before the first MFMA; every tile's sum in the same order: the same bits)
-  auto in_compute = [&](int c0, const f32x4 (&xa)[UMAX][4], const f32x4 (&wb)[UMAX][4], int cbuf) {
+  auto in_compute = [&](int c0, const f32x4 (&xa)[UMAX][4], const f32x4 (&wb)[UMAX][4], float* dst) {
     const int nck = min(NCM, t_hi - c0);
     f32x4 acc[UMAX], ce[UMAX][3];
 #pragma unroll
@@ -473,14 +496,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int t = c0 + cc;
       if (wsq_any) maxnorm_div(0, acc[j]);
       const f32x4 y = epi_c(ce[j][0], ce[j][1], ce[j][2], acc[j]);
-      *(f32x4*)(act + cbuf * slab + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = y;
+      *(f32x4*)(dst + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = y;
     }
   };
-  auto in_layer = [&](int64_t rbase, int cbuf, int cfrom) {
+  auto in_layer = [&](int64_t rbase, float* dst, int cfrom) {
     for (int c0 = cfrom; c0 < t_hi; c0 += NCM) {
       f32x4 xa[UMAX][4], wb[UMAX][4];
       in_issue(rbase, c0, xa, wb);
-      in_compute(c0, xa, wb, cbuf);
+      in_compute(c0, xa, wb, dst);
     }
   };
 
@@ -493,7 +516,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int OGH = 8;
   f32x4 ow0[OGH], ow1[OGH];
   auto out_wpre = [&]() {
-    const int oo = ((RT * NDT * r) / n) % NDT;
+    const int oo = (((PAIR ? 2 : 1) * RT * NDT * r) / n) % NDT;
     const __amdgpu_buffer_rsrc_t r4 = p3d_rsrc(lo.Wf);
 #pragma unroll
     for (int g = 0; g < OGH; ++g) {
@@ -516,11 +539,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #else
 #define P3D_S6_OSTAMP(k) do { } while (0)
 #endif
-  auto out_phase = [&](int64_t orow0) {
-    constexpr int OT = RT * NDT;
-    const int o_lo = (OT * r) / n, o_hi = (OT * (r + 1)) / n;
+  // (PAIR: both units' tiles, A's then B's, dealt over the members as one list)
+  auto out_phase = [&](int64_t orow0, int64_t orow1) {
+    constexpr int OT = RT * NDT, OTT = PAIR ? 2 * OT : OT;
+    const int o_lo = (OTT * r) / n, o_hi = (OTT * (r + 1)) / n;
     P3D_S6_OSTAMP(0);
-    const __amdgpu_buffer_rsrc_t ry = p3d_rsrc(act + 3 * slab), r4 = p3d_rsrc(lo.Wf);
+    const __amdgpu_buffer_rsrc_t ryA = p3d_rsrc(act + 3 * slab), r4 = p3d_rsrc(lo.Wf);
+    const __amdgpu_buffer_rsrc_t ryB = p3d_rsrc(act + (PAIR ? 7 : 3) * slab);
     for (int c0 = o_lo; c0 < o_hi; c0 += OCH) {
       const int nt = min(OCH, o_hi - c0);
       f32x4 oacc[OCH];
@@ -529,7 +554,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < OCH; ++j) {
         if (j >= nt) break;                    // (workgroup-uniform)
-        const int tile = c0 + j, ort = tile / NDT, oo = tile % NDT;
+        const bool tb = PAIR && c0 + j >= OT;    // (workgroup-uniform)
+        const int tile = tb ? c0 + j - OT : c0 + j, ort = tile / NDT, oo = tile % NDT;
+        const __amdgpu_buffer_rsrc_t ry = tb ? ryB : ryA;
         // the K slice in halves of 8 k-groups, both halves' fragments requested before the first
         // MFMA (32 loads at L = 1024: the hidden rings are dead here; two 8-entry arrays stay in
         // registers where one 16-entry array went to scratch)
@@ -579,7 +606,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int k = 1; k < 4; ++k) tot += sl[k];
         if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
-        p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
+        if (PAIR && c0 + w >= OT) p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w - OT) * 64 + lane, orow1);
+        else p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
       }
       if (c0 == o_lo) P3D_S6_OSTAMP(2);
       __syncthreads();                         // red is rewritten next (next round / phase)
@@ -598,11 +626,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
+  if constexpr (!PAIR) {
   int c0b = 0;
   if (gi < p.nb) {                           // the group's first step: its input layer alone
-    if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, 0);
+    if (t_lo < t_hi) in_compute(t_lo, xa0, wb0, act);
     P3D_S6_STAMP(trs, 5);
-    in_layer((int64_t)gi * ROWS, 0, t_lo + NCM);
+    in_layer((int64_t)gi * ROWS, act, t_lo + NCM);
     P3D_S6_STAMP(trs, 2);
     if (t_lo < t_hi) b_prefetch(1, t_lo);
     group_sync(false);
@@ -790,7 +819,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (c0 + NCM < t_hi) __syncthreads();
       }
       // the next step's input layer (it depends on nothing of this step) in the last phase
-      if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, c0n, t_lo);
+      if (lastp && has_next) in_layer(row0 + (int64_t)ng * ROWS, act + c0n * slab, t_lo);
       if (P3D_S6_OUT_PRE && lastp) out_wpre();
       if (lastp) P3D_S6_OSTAMP(3);
       P3D_S6_STAMP(trs, 8 * ph + 3);
@@ -800,13 +829,258 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       group_sync(false);
       P3D_S6_STAMP(trs, 8 * ph + 4);
     }
-    out_phase(row0);                         // this step's output layer
+    out_phase(row0, 0);                      // this step's output layer
 #ifdef P3D_TRACE
     if (trs && tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
     if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[20480 + blockIdx.x] = wall_clock64();   // every member's end
 #endif
     trs = false;
     c0b = c0n;
+  }
+  } else {
+  // ---- PAIR: units b (A, slabs 0..3) and b + ng (B, slabs 4..7), phases alternating --------
+  // (a unit past the last row -- an odd count of units -- runs on clamped rows and stores nothing)
+  const int m0 = p3d_tile_owner(gb, n, T);
+  const int cntw = p3d_tile_owner(gb + gcount - 1, n, T) - m0 + 1;
+  // group_sync's wait on its own: this wave's K-slice producers have posted `target`
+  auto wait_for = [&](unsigned target) {
+    if (broken) return;
+    int spin = 0;
+    while (true) {
+      const unsigned v = lane < cntw ? __hip_atomic_load(flags + m0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : target;
+      if (__all((v & 0x7fffffffu) >= target)) {
+        if (__any(v & 0x80000000u)) broken = true;
+        break;
+      }
+      if (++spin > P3D_SERVE_SPIN) {
+        broken = true;
+        if (lane == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  };
+  // this wave's share of a member's post, after its stores are acknowledged (the caller's vmcnt
+  // wait): the fourth wave to count posts the member's flag
+  auto post_wave = [&]() {
+    ++nsync;
+    if (lane == 0) {
+      const int old = __hip_atomic_fetch_add(&sh[6], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((old & 3) == 3)
+        __hip_atomic_store(flags + r, nsync | (broken ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
+  // block s: unit s & 1, hidden phase s / 2 + 1; its operand / output / residual slabs
+  auto slabs = [&](int s, const float*& A, float*& Y, const float*& res) {
+    const int ph = (s >> 1) + 1, cur = (2 * ((ph - 1) >> 1)) % 3, t1 = (cur + 1) % 3, t2 = (cur + 2) % 3;
+    const bool second = ((ph - 1) & 1) == 1;
+    float* base = act + (s & 1) * 4 * slab;
+    A = base + (second ? t1 : cur) * slab;
+    Y = base + (ph == NH ? 3 : (second ? t2 : t1)) * slab;
+    res = (second && p.residual) ? base + cur * slab : nullptr;
+  };
+  const int nck = max(min(NCM, t_hi - t_lo), 1);
+  const int aoff0 = (gb * 64 + lane) * 16, rstride = ngL * 1024, voff = lane * 16;
+  int toff[NCM];
+#pragma unroll
+  for (int cc = 0; cc < NCM; ++cc) toff[cc] = ((t_lo + (cc < nck ? cc : nck - 1)) * ngL + gb) * 1024;
+  f32x4 ra_[DA][RT], rb_[DEPTH][NCM];        // the register ring, loaded for the next block ahead
+  auto ring_load = [&](int layer, const float* A) {
+    const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A), rw = p3d_rsrc(p.ly[layer].Wf);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (d < DA)
+#pragma unroll
+        for (int t = 0; t < RT; ++t) ra_[d][t] = p3d_ld_sc1(ra, aoff0 + t * rstride + d * 1024);
+#pragma unroll
+      for (int cc = 0; cc < NCM; ++cc)
+        rb_[d][cc] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, voff, toff[cc] + d * 1024, 0));
+      // slot order kept: the first MFMAs wait for slot 0 only (the scheduler had issued a slot-0
+      // fragment last, and the contraction then waited for every request in flight)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Every memory request of a block is unconditional (the last block requests a ring it does not
+  // use, every wave stores all its epilogue tiles -- a clamped duplicate where it has fewer, the
+  // same bits), and the previous block's post sits in a peeled first ring round: requests on
+  // branches left the compiler's vmcnt accounting at a merge it resolved with full drains (the
+  // first build waited for everything in flight before every contraction and every store).
+  for (int b = gi; b < p.nb; b += 2 * ng) {
+    const int64_t rowA = (int64_t)b * ROWS, rowB = (int64_t)(b + ng) * ROWS;
+    // input layers: both units' operands requested at once, A's computed, B's, one post for both
+    // (the first: binds the bank); block 0's first post then carries nothing new (the count stays
+    // one post per block)
+    {
+      f32x4 xa[UMAX][4], wa[UMAX][4], xb[UMAX][4], wbb[UMAX][4];
+      in_issue(rowA, t_lo, xa, wa);
+      in_issue(rowB, t_lo, xb, wbb);
+      in_compute(t_lo, xa, wa, act);
+      P3D_S6_STAMP(trs, 5);
+      in_compute(t_lo, xb, wbb, act + 4 * slab);
+      P3D_S6_STAMP(trs, 2);
+      group_sync(false, false);
+    }
+    wait_for(nsync);                         // the input layers from this wave's K-slice producers
+    P3D_S6_STAMP(trs, 3);
+    {
+      const float *A0, *r0;
+      float* Y0;
+      slabs(0, A0, Y0, r0);
+      ring_load(1, A0);
+    }
+    // The epilogue of block sp: its K slices (red buffer sp & 1) and its tiles' constants requested
+    // (epi_rd), then summed in slice order, finished with the residual operands rv and stored (epi_st)
+    f32x4 part[UMAX][4], ce[UMAX][3], rv[UMAX];
+    auto epi_rd = [&](int sp) {
+      const int php = (sp >> 1) + 1;
+      const f32x4* rdp = red + (sp & 1) * (4 * RT * NCM * 64);
+#pragma unroll
+      for (int j = 0; j < UMAX; ++j) {
+        const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[j][k] = rdp[((k * RT + rt) * NCM + cc) * 64 + lane];
+        const int t = t_lo + (cc < nck ? cc : nck - 1);
+        const float* e = ec + (php * ECT + (t - t_lo)) * 48 + q4;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ce[j][k] = *(const f32x4*)(e + 16 * k);
+      }
+    };
+    auto epi_st = [&](int sp) {
+      const int php = (sp >> 1) + 1;
+      const float *Ap, *resp;
+      float* Yp;
+      slabs(sp, Ap, Yp, resp);
+      f32x4 sacc[UMAX];
+#pragma unroll
+      for (int j = 0; j < UMAX; ++j) {
+        sacc[j] = part[j][0];                // slice 0, tile (rt, cc), then 1, 2, 3
+#pragma unroll
+        for (int k = 1; k < 4; ++k) sacc[j] += part[j][k];
+      }
+      if (wsq_any)
+#pragma unroll
+        for (int j = 0; j < UMAX; ++j) maxnorm_div(php, sacc[j]);
+#pragma unroll
+      for (int j = 0; j < UMAX; ++j) {
+        // (a wave with fewer tiles, or a member with fewer than NCM, stores a clamped duplicate:
+        // the same tile's sum from the same LDS slices and constants, i.e. the same bits)
+        const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+        const int t = t_lo + (cc < nck ? cc : nck - 1);
+        f32x4 yv = epi_c(ce[j][0], ce[j][1], ce[j][2], sacc[j]);
+        if (resp) yv += rv[j];
+        *(f32x4*)(Yp + ((int64_t)(rt * ngL + t) * 64 + lane) * 4) = yv;
+      }
+    };
+    // Block s.  The register ring runs on across blocks: the last DEPTH k-groups refill their slots
+    // with the NEXT block's first DEPTH k-groups (the other unit's previous phase, posted about a
+    // contraction ago, its producers' flags checked one round earlier), so a block starts with its
+    // ring full and the boundary between contractions is the K-combine and epilogue alone.  (A first
+    // form requested the next ring after the contraction: 28 requests per wave in a burst, the
+    // CU's address path busy ~1 us between contractions.)
+    for (int s = 0; s < 2 * NH; ++s) {
+      const int ph = (s >> 1) + 1;
+      const ServeLayer& ly = p.ly[ph];
+      const float *A, *res;
+      float* Y;
+      slabs(s, A, Y, res);
+      const __amdgpu_buffer_rsrc_t ra = p3d_rsrc(A), rw = p3d_rsrc(ly.Wf);
+      P3D_S6_STAMP(trs, 8 + 4 * s);
+      f32x4 acc[NCM][RT];
+#pragma unroll
+      for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[cc][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto mfmas = [&](int d) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+            for (int t = 0; t < RT; ++t)
+              acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d][t][e], acc[cc][t], 0, 0, 0);
+      };
+      // slot d refilled with k-group g of the operands (ra2, rw2)
+      auto refill = [&](int d, const __amdgpu_buffer_rsrc_t& ra2, const __amdgpu_buffer_rsrc_t& rw2, int g) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) ra_[d][t] = p3d_ld_sc1(ra2, aoff0 + t * rstride + g * 1024);
+#pragma unroll
+        for (int cc = 0; cc < NCM; ++cc)
+          rb_[d][cc] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw2, voff, toff[cc] + g * 1024, 0));
+      };
+      auto round = [&](int g0) {             // DEPTH k-groups, each slot refilled DEPTH ahead
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+          mfmas(d);
+          refill(d, ra, rw, g0 + DEPTH + d);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      round(0);
+      // the previous block's post (block 0: nothing new -- one post per block): its stores were issued
+      // before this round's DEPTH (RT + NCM) refills, so a wait down to that many leaves the refills in
+      // flight (vmcnt retires in issue order) and finds the stores acknowledged
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH * (RT + NCM)) : "memory");
+      post_wave();
+      __builtin_amdgcn_sched_barrier(0);
+      for (int g0 = DEPTH; g0 < gcount - 2 * DEPTH; g0 += DEPTH) round(g0);
+      // the next block's producers (the other unit's previous phase; the last block: its own unit's,
+      // there too): flags requested a round ahead of the check
+      const unsigned fl = __hip_atomic_load(flags + m0 + min(lane, cntw - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_sched_barrier(0);
+      round(gcount - 2 * DEPTH);
+      if (!broken) {
+        if (__any(fl & 0x80000000u)) broken = true;
+        else if (!__all((fl & 0x7fffffffu) >= nsync)) wait_for(nsync);
+      }
+      // this block's residual operands, then the last DEPTH k-groups, each slot refilled with the
+      // next block's (the last block: its own again, unused)
+      const __amdgpu_buffer_rsrc_t rr = p3d_rsrc(res ? res : A);
+#pragma unroll
+      for (int j = 0; j < UMAX; ++j) {
+        const int u = min(w + 4 * j, RT * NCM - 1), rt = u / NCM, cc = u % NCM;
+        const int t = t_lo + (cc < nck ? cc : nck - 1);
+        rv[j] = p3d_ld_sc1(rr, (int)(((int64_t)(rt * ngL + t) * 64 + lane) * 16));
+      }
+      {
+        const int sn = min(s + 1, 2 * NH - 1);
+        const float *An, *rn;
+        float* Yn;
+        slabs(sn, An, Yn, rn);
+        const __amdgpu_buffer_rsrc_t ran = p3d_rsrc(An), rwn = p3d_rsrc(p.ly[(sn >> 1) + 1].Wf);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+          mfmas(d);
+          refill(d, ran, rwn, d);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      P3D_S6_STAMP(trs, 8 + 4 * s + 1);
+      f32x4* rd = red + (s & 1) * (4 * RT * NCM * 64);
+#pragma unroll
+      for (int cc = 0; cc < NCM; ++cc)
+#pragma unroll
+        for (int t = 0; t < RT; ++t) rd[((w * RT + t) * NCM + cc) * 64 + lane] = acc[cc][t];
+      if (broken) sh[4] = 1;
+      __syncthreads();
+      broken = broken || sh[4] != 0;
+      P3D_S6_STAMP(trs, 8 + 4 * s + 2);
+      epi_rd(s);
+      __builtin_amdgcn_sched_barrier(0);
+      epi_st(s);
+      P3D_S6_STAMP(trs, 8 + 4 * s + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    post_wave();                             // the last block's, at once
+    if (P3D_S6_OUT_PRE) out_wpre();
+    wait_for(nsync);                         // both units' last hidden layers (slabs 3, 7)
+    out_phase(rowA, rowB);
+#ifdef P3D_TRACE
+    if (trs && tr6 && tid == 0) tr6[8 * (NH + 1)] = wall_clock64();
+    if (tid == 0 && blockIdx.x < 1024) g_p3d_trace[20480 + blockIdx.x] = wall_clock64();   // every member's end
+#endif
+    trs = false;
+  }
   }
   if (tid == 0 && sh[5] >= 0)   // (every member has read the epoch by now: see its read)
     __hip_atomic_fetch_add(p.epoch + sh[5], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

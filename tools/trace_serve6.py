@@ -44,9 +44,25 @@ def main():
     t0 = min(t[g, r, 0] for g, r in live)
     us = lambda v: round((v - t0) / 100.0, 2)   # noqa: E731
     out = []
+    pair = os.environ.get("P3D_SERVE6_PAIR", "0") == "1"
     for g, r in live:
         row = t[g, r]
         if row[8 * (NH + 1)] < row[0]:          # stale (a group idle in the last launch)
+            continue
+        if pair:
+            # the pair form's blocks (unit s & 1, phase s // 2 + 1) at 8 + 4 s: contraction start,
+            # contraction end, K-combine barrier passed, epilogue stores issued
+            blk = [[round((row[8 + 4 * s + 1] - row[8 + 4 * s]) / 100, 2),
+                    round((row[8 + 4 * s + 2] - row[8 + 4 * s + 1]) / 100, 2),
+                    round((row[8 + 4 * s + 3] - row[8 + 4 * s + 2]) / 100, 2),
+                    round((row[8 + 4 * (s + 1)] - row[8 + 4 * s + 3]) / 100, 2) if s + 1 < 2 * NH else None]
+                   for s in range(2 * NH)]
+            cyc = sum(row[64 + 8 + 4 * s + 1] - row[64 + 8 + 4 * s] for s in range(2 * NH))
+            wall = sum(row[8 + 4 * s + 1] - row[8 + 4 * s] for s in range(2 * NH))
+            out.append({"group": g, "row": r, "clock_ghz": round(cyc / max(wall, 1) / 10.0, 3), "start": us(row[0]),
+                        "in_a": us(row[5]), "in_b": us(row[2]), "handoff0": us(row[3]), "first_block": us(row[8]),
+                        "last_stores": us(row[8 + 4 * (2 * NH - 1) + 3]), "reduce_end": us(row[8 * (NH + 1)]),
+                        "blocks_us": blk})
             continue
         ph = []
         for p in range(1, NH + 1):
