@@ -244,7 +244,7 @@ struct p3d_model {
   int serve6_split = 0;     // k_serve6 groups per XCD, 0 = chosen per launch (env P3D_SERVE6_SPLIT: 1..8)
   int serve6_rt = 0;        // k_serve6 row tiles per unit, 0 = chosen per launch (env P3D_SERVE6_RT: 4 or 2)
   int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
-  int serve6_pair = 0;      // XCD-wide units of 10 row tiles as two 5-row-tile units run side by side (env P3D_SERVE6_PAIR)
+  int serve6_pair = 1;      // XCD-wide units of 10 row tiles as two 5-row-tile units run side by side (env P3D_SERVE6_PAIR: 0 off)
   std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
   // data-parallel step with the library's own all-reduce (p3d_dp.h)
   p3d_comm* comm = nullptr;      // not owned (p3d_comm_create / p3d_comm_destroy)
@@ -1544,7 +1544,8 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     use6 = plan.S > 0;                       // no form covers this width: k_serve5
     // k_serve6's four activation slabs per group (8 S groups of 16 RT rows) in serve6_act
     if (use6 && (int64_t)8 * plan.S * 16 * plan.rt > P3D_SERVE6_ROWS) use6 = false;
-    // the pair form: an XCD-wide unit of 10 row tiles run as two units of 5 side by side
+    // the pair form: an XCD-wide unit of 10 row tiles run as two units of 5 side by side, phases
+    // alternating (p3d_serve6.h; the same bits; 20 steps: 99.2 vs 101.1 us, six alternating pairs)
     if (use6 && m->serve6_pair && plan.S == 1 && plan.rt == 10 && L / 64 >= 12) {
       plan.rt = 5;
       plan.pair = true;

@@ -198,9 +198,12 @@ def _pmc_files(config):
 
 def _committed_traffic(symbol, config):
     """HBM bytes per launch of `symbol` on `config` (see _pmc_files), or None."""
+    # (k_serve6's single-unit forms are named without the pair flag by p3d_kernel_name; their
+    # symbols carry it: "k_serve6<4, 3, 2, 10>" is "k_serve6<4, 3, 2, 10, false>(ServeArgs)")
+    alt = symbol[:-1] + ", false>" if symbol.startswith("k_serve6<") and symbol.endswith(">") else None
     for d in _pmc_files(config):
         for k, v in d.items():
-            if symbol in k:
+            if symbol in k or (alt and alt in k):
                 return v["hbm_bytes_per_launch"]
     return None
 

@@ -142,15 +142,17 @@ def test_serve_knob_variants_vs_oracle(monkeypatch, split, upm, depth, L, N):
     m.close()
 
 
-def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1, rt=None):
+def _serve6_model(monkeypatch, cfg, split=None, mode=None, seed=1, rt=None, pair=None):
     if split is not None:
         monkeypatch.setenv("P3D_SERVE6_SPLIT", str(split))
     if mode is not None:
         monkeypatch.setenv("P3D_SERVE6", str(mode))
     if rt is not None:
         monkeypatch.setenv("P3D_SERVE6_RT", str(rt))
+    if pair is not None:
+        monkeypatch.setenv("P3D_SERVE6_PAIR", str(pair))
     st, m = make(cfg, seed=seed)
-    for k in ("P3D_SERVE6_SPLIT", "P3D_SERVE6", "P3D_SERVE6_RT"):
+    for k in ("P3D_SERVE6_SPLIT", "P3D_SERVE6", "P3D_SERVE6_RT", "P3D_SERVE6_PAIR"):
         monkeypatch.delenv(k, raising=False)
     return st, m
 
@@ -160,16 +162,21 @@ def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
     batch-64 units (16-column tiles dealt contiguously, 7 tiles per CU at 3 groups) and 32-row
     half-step units at 5 (and 3) groups per XCD, and XCD-wide units of 6 / 8 / 16 row tiles give
     the same bits -- the association of every sum is fixed by the tile, not by the group or unit
-    shape -- and the oracle's outputs; the auto choice for 20 steps is one unit of 160 rows per
-    XCD on all 32 of its CUs, 2 column tiles each."""
+    shape -- and the oracle's outputs; the auto choice for 20 steps is 160 rows per XCD on all 32
+    of its CUs, 2 column tiles each: one unit, or (the pair form, P3D_SERVE6_PAIR) two 80-row units
+    with alternating phases -- both forms run here, the same bits."""
     import _p3d
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     B = 64 * 20
     x = np.random.default_rng(620).standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
     outs = {}
-    for split, rt in ((None, None), (1, 4), (2, 4), (3, 4), (4, 4), (5, 2), (3, 2), (1, 6), (1, 8), (1, 16)):
-        st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
+    for split, rt in ((None, None), (1, 4), (2, 4), (3, 4), (4, 4), (5, 2), (3, 2), (1, 6), (1, 8), (1, 16),
+                      ("pair0", None), ("pair1", None)):
+        if isinstance(split, str):
+            st, m = _serve6_model(monkeypatch, cfg, pair=int(split[-1]))
+        else:
+            st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
         y = m.serve_device(xd)
         torch.cuda.synchronize()
         m.serve_check()
@@ -179,7 +186,10 @@ def test_serve6_every_split_same_bits_and_oracle(monkeypatch):
         outs[(split, rt)] = (y, name.value.decode())
         m.close()
     auto = outs[(None, None)]
-    assert auto[1] == "k_serve6<4, 3, 2, 10>", auto[1]     # 20 steps -> one 160-row unit per XCD
+    # 20 steps -> 160 rows per XCD: one unit, or two of 80 side by side (the pair form)
+    assert outs[("pair0", None)][1] == "k_serve6<4, 3, 2, 10>", outs[("pair0", None)][1]
+    assert outs[("pair1", None)][1] == "k_serve6<4, 3, 2, 5, true>", outs[("pair1", None)][1]
+    assert auto[1] in ("k_serve6<4, 3, 2, 10>", "k_serve6<4, 3, 2, 5, true>"), auto[1]
     assert outs[(3, 4)][1] == "k_serve6<2, 3, 7, 4>", outs[(3, 4)][1]
     for key, (y, _) in outs.items():
         assert torch.equal(y, auto[0]), key
@@ -211,11 +221,13 @@ def test_serve6_launch_sizes_vs_oracle(B):
     (1024, 2, True, True, False, True),      # --predict_14
     (2048, 1, True, True, False, False),     # 128 tiles: 13 per CU at 3 groups -> two contractions
 ])
-@pytest.mark.parametrize("split,rt", [(None, None), (3, 4), (5, 2), (1, 10)])
-def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split, rt):
+@pytest.mark.parametrize("split,rt,pair", [(None, None, None), (3, 4, None), (5, 2, None), (1, 10, 0), (1, 10, 1)])
+def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_norm, p14, split, rt, pair):
+    """(rt 10 with pair 1: the pair form where the width allows it (L >= 768), 17 units of 80 rows --
+    a group runs two pairs, the last unit's partner past the last row)"""
     cfg = ref_mlp.Cfg(linear_size=L, num_layers=N, residual=residual, batch_norm=batch_norm, max_norm=max_norm,
                       predict_14=p14)
-    st, m = _serve6_model(monkeypatch, cfg, split, rt=rt)
+    st, m = _serve6_model(monkeypatch, cfg, split, rt=rt, pair=pair)
     B = 64 * 20 + 5
     x = np.random.default_rng(L + N).standard_normal((B, 32)).astype(np.float32)
     y = m.serve_device(torch.from_numpy(x).cuda()).cpu().numpy()
@@ -225,8 +237,9 @@ def test_serve6_variants_vs_oracle(monkeypatch, L, N, residual, batch_norm, max_
     m.close()
 
 
-@pytest.mark.parametrize("split,rt", [(1, 4), (2, 4), (3, 4), (5, 2), (1, 10)])
-def test_serve6_many_steps_per_group(monkeypatch, split, rt):
+@pytest.mark.parametrize("split,rt,pair", [(1, 4, None), (2, 4, None), (3, 4, None), (5, 2, None), (1, 10, 0),
+                                           (1, 10, 1)])
+def test_serve6_many_steps_per_group(monkeypatch, split, rt, pair):
     """k_serve6 forced on a long launch (P3D_SERVE6=2): every group runs many steps, so the
     next step's input layer rides in the last phase and each step's output layer runs as its own
     phase after that hand-off (tiles dealt over the members); every row vs the oracle / k_serve5."""
@@ -234,7 +247,7 @@ def test_serve6_many_steps_per_group(monkeypatch, split, rt):
     B = 64 * 300 + 9
     x = np.random.default_rng(77 + split).standard_normal((B, 32)).astype(np.float32)
     xd = torch.from_numpy(x).cuda()
-    st, m6 = _serve6_model(monkeypatch, cfg, split, mode=2, rt=rt)
+    st, m6 = _serve6_model(monkeypatch, cfg, split, mode=2, rt=rt, pair=pair)
     y6 = m6.serve_device(xd)
     torch.cuda.synchronize()
     m6.serve_check()

@@ -22,9 +22,10 @@ LIB = os.path.join(ROOT, "3d-pose-baseline_amd", "libp3d.so")
 # the kernels on the default paths (rocprof names); every one must be spill- and scratch-free
 HOT = [
     "void k_gemv_chain<4, 4>(GemvChain)",            # batch <= 4 forward, one launch
-    "void k_serve6<4, 3, 2, 10>(ServeArgs)",          # the headline: 20 batch-64 requests per launch
-    "void k_serve6<4, 3, 2, 1>(ServeArgs)",           # one batch-64 request
-    "void k_serve6<4, 3, 2, 2>(ServeArgs)",
+    "void k_serve6<4, 3, 2, 5, true>(ServeArgs)",     # the headline: 20 batch-64 requests per launch (pair form)
+    "void k_serve6<4, 3, 2, 10, false>(ServeArgs)",   # the same rows as one 160-row unit per XCD (P3D_SERVE6_PAIR=0)
+    "void k_serve6<4, 3, 2, 1, false>(ServeArgs)",           # one batch-64 request
+    "void k_serve6<4, 3, 2, 2, false>(ServeArgs)",
     "void k_gemm_bf16p<64, 4, 8, false, 0, false>",   # cfg5 hidden layer
     "k_wgrad_multi",                      # cfg3 weight gradients + fused TF1 Adam
     "k_adam_pack",                                    # DP optimizer
