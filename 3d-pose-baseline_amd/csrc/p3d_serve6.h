@@ -462,6 +462,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
     }
+    asm volatile("" ::: "memory");           // (the producers' data is read after the relaxed flag check)
   };
 
   // input layer (K0 = input_size <= 64) of the member's tiles for the rows of the step at
@@ -859,6 +860,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         break;
       }
     }
+    asm volatile("" ::: "memory");           // (as in group_sync)
   };
   // this wave's share of a member's post, after its stores are acknowledged (the caller's vmcnt
   // wait): the fourth wave to count posts the member's flag
@@ -1032,6 +1034,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (__any(fl & 0x80000000u)) broken = true;
         else if (!__all((fl & 0x7fffffffu) >= nsync)) wait_for(nsync);
       }
+      // (the flags are relaxed atomics: nothing in the memory model keeps the compiler from hoisting
+      // the next block's operand loads above the check -- this does; the hardware issues them after
+      // the flag values are in hand)
+      asm volatile("" ::: "memory");
       // this block's residual operands, then the last DEPTH k-groups, each slot refilled with the
       // next block's (the last block: its own again, unused)
       const __amdgpu_buffer_rsrc_t rr = p3d_rsrc(res ? res : A);
