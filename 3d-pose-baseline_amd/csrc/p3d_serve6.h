@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // activation ring depth (the wide forms cannot hold both rings DEPTH deep: 4 x 11 fragments
   // spilled 77 registers at NCM = 7, RT = 4)
 #ifndef P3D_S6_DA
-  constexpr int DA = RT >= 6 ? (DEPTH >= 8 ? 4 : 2) : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);
+  // (PAIR: every slot holds both operands -- the ring runs on across blocks)
+  constexpr int DA = PAIR ? DEPTH : RT >= 6 ? (DEPTH >= 8 ? 4 : 2) : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);
 #else
   constexpr int DA = RT >= 6 ? P3D_S6_DA : (NCM >= 7 && DEPTH > 2 ? 2 : DEPTH);   // (development builds)
 #endif

@@ -34,7 +34,7 @@ def main():
     torch.manual_seed(0)
     out = {"cases": []}
     ok = True
-    for B in (1280, 1200, 1100, 1281 - 64, 64 * 20):
+    for B in (1280, 1200, 1100, 1281 - 64, 64 * 20, 1024, 1000, 960):
         x = torch.randn((B, 32), device="cuda")
         y0 = m0.serve_device(x).clone()
         ys = [m1.serve_device(x).clone() for _ in range(3)]
