@@ -345,327 +345,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_gemm_bf16p(GemmBf16Args p) {
   }
 }
 
-typedef unsigned p3d_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t p3d_bf16s_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-// =====================================================================================
-// K split over the 4 waves of a 128 x 128 tile, operands loaded straight into registers
-// (k_gemm_bf16d, round 5).
-//
-// Why: k_gemm_bf16p is bound by its operand intake -- 2 MB per CU per layer through LDS-DMA,
-// whose per-CU rate tops out near 70 GB/s; the PMC pass of the cfg5 step put the CU's texture
-// addresser (TA) busy 0.76 of the kernel (profiles/r05_v1_pmc_units_stress.json) against MFMA
-// busy 0.27.  Register loads of hand-off data reach ~110-120 GB/s per CU (MI355X_MICROARCH.md,
-// handoff-payload).  Splitting the tile's K over the waves (not its rows or columns) keeps every
-// operand byte loaded ONCE per CU: wave w takes k-groups [ngA w / 4, ngA (w+1) / 4) of all 8 row
-// tiles and all 8 column tiles -- per k-group 16 fragments (16 KB) for 64 MFMAs into a 128 x 128
-// fp32 accumulator (256 AGPRs at one wave per SIMD, 512 registers), the next D - 1 k-groups' 16
-// fragments in flight (a D-deep register ring).  The four K-slice sums meet in LDS as
-// ((s0 + s2) + (s1 + s3)) -- one fixed association -- then the fused epilogue of k_gemm_bf16p.
-// =====================================================================================
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm_bf16d(GemmBf16Args p) {
-  constexpr int ES = 132;                                    // fp32 tile row stride in LDS
-  __shared__ __attribute__((aligned(16))) float red[2 * 128 * ES];
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tiles_n = p.N / 128, tiles_m = p.M / 128;
-  const int GM = (tiles_m % 4 == 0) ? 4 : ((tiles_m % 2 == 0) ? 2 : 1);
-  const int grp = tile_id / (GM * tiles_n), in_grp = tile_id % (GM * tiles_n);
-  const int mt = grp * GM + (in_grp % GM), nt = in_grp / GM;
-  const int ngA = p.K / 32;
-  const int kb = (ngA * w) >> 2, nk = ((ngA * (w + 1)) >> 2) - kb;   // this wave's k-groups (nk % D == 0)
-  const __amdgpu_buffer_rsrc_t ra = p3d_bf16s_rsrc((const unsigned char*)p.A + (int64_t)(8 * mt) * ngA * 1024);
-  const __amdgpu_buffer_rsrc_t rb = p3d_bf16s_rsrc((const unsigned char*)p.Bt + (int64_t)(8 * nt) * ngA * 1024);
-  const int voff = lane * 16;
-  bf16x8 fa[D][8], fb[D][8];
-  auto load = [&](int d, int g) {   // k-group kb + g of all 8 row tiles and all 8 column tiles
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      fa[d][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, (j * ngA + kb + g) * 1024, 0));
-      fb[d][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, voff, (j * ngA + kb + g) * 1024, 0));
-    }
-  };
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mfmas = [&](int d) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[d][r], fb[d][c], acc[r][c], 0, 0, 0);
-  };
-#pragma unroll
-  for (int d = 0; d < D; ++d) load(d, d);
-  for (int g0 = 0; g0 < nk - D; g0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      mfmas(d);
-      load(d, g0 + D + d);
-      __builtin_amdgcn_sched_barrier(0);    // the refill of slot d stays ahead of slot d + 1's MFMAs
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < D; ++d) mfmas(d);
-  // ---- K slices: waves 2, 3 hand theirs to waves 0, 1 (s0 + s2, s1 + s3), then both halves ----
-  const int i = lane & 15, q = lane >> 4;
-  auto put = [&](float* et) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) et[(16 * r + 4 * q + e) * ES + 16 * c + i] = acc[r][c][e];
-  };
-  if (w >= 2) put(red + (w - 2) * 128 * ES);
-  __syncthreads();
-  if (w < 2) {                               // in place: half w = s_w + s_(w+2)
-    float* et = red + w * 128 * ES;
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = (16 * r + 4 * q + e) * ES + 16 * c + i;
-          et[k] = acc[r][c][e] + et[k];
-        }
-  }
-  __syncthreads();
-  // ---- epilogue (k_gemm_bf16p's): element = half 0 + half 1, bias / BN / ReLU / residual ----
-  const int ngY = p.N / 32;
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int item = it * 256 + tid;
-    const int chunk = item >> 6, l = item & 63;
-    const int rl = 16 * (chunk >> 2) + (l & 15);
-    const int cl = 32 * (chunk & 3) + 8 * (l >> 4);
-    const int row = 128 * mt + rl, col = 128 * nt + cl;
-    const int64_t off = p3d_pk16(row, col, ngY);
-    u16x8 rv;
-    if (p.res) rv = *(const u16x8*)(p.res + off);
-    u16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int n = col + e;
-      const float s = red[rl * ES + cl + e] + red[128 * ES + rl * ES + cl + e];
-      float z = s + p.epi.bias[n];
-      float y = p.epi.inv ? z * p.epi.inv[n] + p.epi.shift[n] : z;
-      if (p.epi.relu) y = fmaxf(y, 0.0f);
-      if (p.res) y += p3d_bf2f(rv[e]);
-      o[e] = p3d_f2bf(y);
-    }
-    *(u16x8*)(p.Y + off) = o;
-  }
-}
-
-// =====================================================================================
-// Split-K form for wide layers at modest M (cfg5: M = 1024, N = K = 4096).
-//
-// Why: the 128 x 128 tile of k_gemm_bf16p needs 32 KB of operands per 64-deep k-step for
-// 2 MFLOP; its 8 waves (64 x 32 each) read 96 KB of fragments from LDS per k-step and the
-// LDS-DMA writes another 32 KB -- the LDS array (256 B/clk/CU) is as busy as the MFMA pipes.
-// A 256 x 128 tile with 64 x 64 per wave does twice the MFMA work per k-step for 48 KB of
-// operands and 128 KB of fragment reads (LDS 2/3 busy, 25 % fewer L2->CU bytes per FLOP).
-// At M = 1024 such tiles number only 4 x 32 = 128, so each tile's K is split in two halves
-// run by two workgroups: 256 workgroups, one per CU.
-//
-// The halves meet in one launch (no second kernel, no fp32 partial round trip through a
-// separate reduction pass): workgroups [0, T) take the upper K half ("writers"), [T, 2T) the
-// lower ("readers").  A writer stores its fp32 accumulators write-through (sc1) to a
-// per-tile partial slot, every wave drains (vmcnt 0), a barrier, then one lane stores the
-// tile's flag = this launch's tag (sc1).  A reader, after its own half, polls the flag (sc1
-// load), barriers, loads the partial with sc1 loads and forms acc_lo + acc_hi -- always this
-// association, so every run gives the same bits -- then the fused epilogue.  This is the
-// first hand-off row of MI355X_MICROARCH.md's sc1 table (hipMalloc memory, one workgroup per
-// CU, 16-B sc1 stores and loads).  Tags: each tile has an epoch word read by both halves at
-// kernel start; tag = epoch + 1; the reader adds 1 to the epoch after its poll matched (the
-// writer read the epoch before it could publish), so tags are unique per launch with no
-// memset in front, graph replays included.  No deadlock whatever the residency: every writer
-// has a lower workgroup id than every reader, so the dispatcher places all writers before any
-// reader, and writers wait for nothing.  The poll is bounded and reports through *err.
-// =====================================================================================
-// 16-B sc1 load (L1 bypassed): the partial another workgroup stored write-through
-__device__ __forceinline__ f32x4 p3d_bf16s_ld(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
-}
-
-struct GemmBf16SplitArgs {
-  GemmBf16Args g;
-  float* part;          // [tiles][8 waves][16 fragments][64 lanes] f32x4
-  unsigned* sync;       // [tiles][2][32]: epoch word, flag word (own 128-B lines)
-  int* err;
-};
-
-#define P3D_BF16S_SPIN (1 << 22)
-
-template <int NST>
-__global__ __launch_bounds__(512) void k_gemm_bf16s(GemmBf16SplitArgs sa) {
-  constexpr int KG = 2;                             // BK = 64
-  constexpr int AT = 16, BT = 8;                    // 16-row tiles of A, 16-column tiles of B per stage k-group
-  constexpr int STAGE = (AT + BT) * KG * 1024;      // 48 KB
-  constexpr int EPI = 256 * 132 * 4;
-  constexpr int LDS = (NST * STAGE > EPI) ? NST * STAGE : EPI;
-  constexpr int PER = (AT + BT) * KG / 8;           // LDS-DMA instructions per wave per stage (6)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
-  const GemmBf16Args& p = sa.g;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;                // 4 x 2 waves of 64 x 64
-  const int tiles_n = p.N / 128, tiles_m = p.M / 256, T = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const bool reader = bid >= T;
-  const int lb = reader ? bid - T : bid;
-  // XCD-aware remap within each half (bijective for any T), then GM x (32 / GM) blocks
-  const int q8 = T / 8, r8 = T % 8, xcd = lb % 8;
-  const int tile_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lb / 8;
-  const int GM = (tiles_m % 4 == 0) ? 4 : ((tiles_m % 2 == 0) ? 2 : 1);
-  const int grp = tile_id / (GM * tiles_n), in_grp = tile_id % (GM * tiles_n);
-  const int mt = grp * GM + (in_grp % GM), nt = in_grp / GM;
-  const int tile = mt * tiles_n + nt;
-  const int ngA = p.K / 32;
-  const int nks = p.K / 128;                        // k-steps per half
-  const int ks0 = reader ? 0 : nks;
-  unsigned* epoch = sa.sync + tile * 64;
-  unsigned* flag = epoch + 32;
-  unsigned tag = 0;
-  if (tid == 0) tag = __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  const unsigned char* Ag = (const unsigned char*)p.A + (int64_t)(16 * mt) * ngA * 1024;
-  const unsigned char* Bg = (const unsigned char*)p.Bt + (int64_t)(8 * nt) * ngA * 1024;
-
-  auto issue = [&](int ks, int buf) {
-    unsigned char* base = smem + buf * STAGE;
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      const int t = w * PER + c;                    // 0 .. 47
-      const bool isB = t >= AT * KG;
-      const int tt = isB ? t - AT * KG : t;
-      const int j = tt / KG, g = tt % KG;
-      const unsigned char* src = (isB ? Bg : Ag) + ((int64_t)j * ngA + (ks0 + ks) * KG + g) * 1024 + lane * 16;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + t * 1024), 16, 0, 0);
-    }
-  };
-  auto read = [&](int buf, int g, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
-    const unsigned char* base = smem + buf * STAGE;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) af[r] = *(const bf16x8*)(base + ((4 * wm + r) * KG + g) * 1024 + lane * 16);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      bfr[c] = *(const bf16x8*)(base + (AT * KG + (4 * wn + c) * KG + g) * 1024 + lane * 16);
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[2][4], fb[2][4];
-
-#pragma unroll
-  for (int s0 = 0; s0 < NST - 1; ++s0)
-    if (s0 < nks) issue(s0, s0);
-  {
-    const int later = (nks - 1) < (NST - 2) ? (nks - 1) : (NST - 2);
-    p3d_wait_stages<PER, NST>(later);
-    __builtin_amdgcn_s_barrier();
-    read(0, 0, fa[0], fb[0]);
-  }
-  int cur = 0;
-  for (int ks = 0; ks < nks; ++ks) {
-    const int buf = ks % NST;
-    if (ks + NST - 1 < nks) issue(ks + NST - 1, (ks + NST - 1) % NST);
-#pragma unroll
-    for (int g = 0; g < KG; ++g) {
-      const int nxt = cur ^ 1;
-      if (g + 1 < KG) {
-        read(buf, g + 1, fa[nxt], fb[nxt]);
-      } else if (ks + 1 < nks) {
-        const int later = (nks - 2 - ks) < (NST - 2) ? (nks - 2 - ks) : (NST - 2);
-        p3d_wait_stages<PER, NST>(later);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        read((ks + 1) % NST, 0, fa[nxt], fb[nxt]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][r], fb[cur][c], acc[r][c], 0, 0, 0);
-      cur = nxt;
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const __amdgpu_buffer_rsrc_t rp = p3d_bf16s_rsrc(sa.part);
-  const int pbase = ((tile * 8 + w) * 16) * 1024 + lane * 16;   // byte offset of fragment 0
-  if (!reader) {
-    // ---- writer: publish the upper half's accumulators, then the flag --------------------
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(p3d_u32x4, acc[r][c]), rp, pbase + (r * 4 + c) * 1024, 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // ---- reader: wait for the upper half, add it (lower + upper), fused epilogue ----------
-  if (w == 0) {
-    const unsigned t0 = __builtin_amdgcn_readfirstlane(tag);
-    bool ok = false;
-    for (int spin = 0; spin < P3D_BF16S_SPIN; ++spin) {
-      const unsigned v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v == t0) { ok = true; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (lane == 0) {
-      if (!ok) __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[r][c] = acc[r][c] + p3d_bf16s_ld(rp, pbase + (r * 4 + c) * 1024);
-  float* et = (float*)smem;
-  const int i = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) et[(64 * wm + 16 * r + 4 * q + e) * 132 + 64 * wn + 16 * c + i] = acc[r][c][e];
-  __syncthreads();
-  const int ngY = p.N / 32;
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int item = it * 512 + tid;        // 64 chunks (16 row tiles x 4 col groups) x 64 lanes
-    const int chunk = item >> 6, l = item & 63;
-    const int rl = 16 * (chunk >> 2) + (l & 15);
-    const int cl = 32 * (chunk & 3) + 8 * (l >> 4);
-    const int row = 256 * mt + rl, col = 128 * nt + cl;
-    const int64_t off = p3d_pk16(row, col, ngY);
-    u16x8 rv;
-    if (p.res) rv = *(const u16x8*)(p.res + off);
-    u16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int n = col + e;
-      float z = et[rl * 132 + cl + e] + p.epi.bias[n];
-      float y = p.epi.inv ? z * p.epi.inv[n] + p.epi.shift[n] : z;
-      if (p.epi.relu) y = fmaxf(y, 0.0f);
-      if (p.res) y += p3d_bf2f(rv[e]);
-      o[e] = p3d_f2bf(y);
-    }
-    *(u16x8*)(p.Y + off) = o;
-  }
-}
+// (round 5 built two more hidden-layer forms here and measured both slower than k_gemm_bf16p in
+// the cfg5 step: k_gemm_bf16s, 256 x 128 tiles with K split over two workgroups meeting in the
+// launch, and k_gemm_bf16d, K split over a 128 x 128 tile's 4 waves with operands straight into
+// registers; round 6 removed both from the product; the sources stay in the history)
 
 // (the round-3 ablation kernels k_gemm_bf16k / k_gemm_bf16w live in tools/bf16_dev_kernels.h)
 

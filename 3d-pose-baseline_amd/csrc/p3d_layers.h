@@ -1,6 +1,6 @@
 // p3d_layers.h -- the layer kernels of the fused training / batch-64 inference paths (gfx950):
-// TF1 Adam primitives, k_fwd / k_fwd_t / k_out_part, the BN-train exchange and split forms, k_dgrad,
-// k_bn_bwd, the weight-gradient kernels (k_wgrad, k_wgrad_multi, k_wgrad_grad, k_dgrad_wg), k_adam_pack,
+// TF1 Adam primitives, k_fwd / k_out_part, the BN-train exchange and split forms, k_dgrad,
+// k_bn_bwd, the weight-gradient kernels (k_wgrad, k_wgrad_multi, k_wgrad_grad), k_adam_pack,
 // the weight (un)packing, k_mse and the max-norm helpers.  Device code only; included by p3d.hip (the
 // host side) and by tools/kdev.hip (single-kernel resource builds: a kernel's registers and spills in
 // seconds instead of the whole library's minutes).
@@ -474,94 +474,6 @@ __global__ __launch_bounds__(64) void k_out_part(OutPartArgs p) {
 }
 
 // =====================================================================================
-// Inference layer in the transposed-accumulator form (p3d_core SWAP): lane (i, q) ends
-// holding row 16s + i, columns n0 + 4q .. +3 -- one float4 per operand of the epilogue
-// (bias, eval BN, residual, packed output: one 1 KB wave store per tile) and one Philox
-// block per lane for dropout.  Same contraction and reduction order as k_fwd (the
-// transposed MFMA sums the same products in the same order), so results are identical.
-// =====================================================================================
-template <int RS, int WK, int DEPTH, int NACC, bool APK, bool YPK, int KIND>
-__global__ __launch_bounds__(64 * WK) void k_fwd_t(FwdArgs p) {
-  __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int ct = blockIdx.x, m0 = blockIdx.y * 16 * RS;
-  const int n0 = ct * 16 + 4 * q;                 // this lane's first column
-  const int ngN = (p.N + 15) >> 4;
-  const bool vec = (p.N & 3) == 0 && n0 + 3 < p.N;
-  // epilogue operands (per-column float4s, per-tile residual) issued before the GEMM
-  f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f}, inv4 = f32x4{1.f, 1.f, 1.f, 1.f}, sh4 = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 rv[RS];
-  uint64_t ctr = p.ctr;
-  if (w == 0) {
-    if (p.ctr_dev) ctr = (uint64_t)*p.ctr_dev;
-    f32x4 g4 = inv4, be4 = sh4, mu4 = sh4, va4 = inv4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = n0 + e < p.N ? n0 + e : p.N - 1;
-      b4[e] = p.bias[c];
-      if (p.bn) { g4[e] = p.gamma[c]; be4[e] = p.beta[c]; mu4[e] = p.mmean[c]; va4[e] = p.mvar[c]; }
-    }
-    if (p.bn) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        inv4[e] = (1.0f / sqrtf(va4[e] + p.eps)) * g4[e];
-        sh4[e] = be4[e] - mu4[e] * inv4[e];
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < RS; ++s) {
-      const int rt = (m0 >> 4) + s;
-      rv[s] = p.res ? *(const f32x4*)(p.res + ((int64_t)rt * ngN + ct) * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  const int ngt = p.K >> 4;
-  const int gb = (ngt * w) / WK, ge = (ngt * (w + 1)) / WK;
-  f32x4 acc[NACC][RS];
-#pragma unroll
-  for (int a = 0; a < NACC; ++a)
-#pragma unroll
-    for (int s = 0; s < RS; ++s) acc[a][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  p3d_core<RS, DEPTH, NACC, APK, true>(p.X, p.ldx, ngt, p.M, m0, p.Wf, ngt, ct, gb, ge, acc);
-  if (!p3d_reduce_waves<RS, NACC, WK>(acc, red)) return;
-  const float mx = p.wsq ? fmaxf(sqrtf(*p.wsq), 1.0f) : 1.0f;
-#pragma unroll
-  for (int s = 0; s < RS; ++s) {
-    const int row = m0 + 16 * s + i;
-    float u[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.keep < 1.0f) {
-      const uint4 wq = p3d_philox(make_uint4((uint32_t)(p.row_off + row), (uint32_t)(n0 >> 2), (uint32_t)p.site,
-                                             (uint32_t)ctr), (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-      const uint32_t xs[4] = {wq.x, wq.y, wq.z, wq.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) u[e] = __uint_as_float((xs[e] & 0x7FFFFFu) | 0x3F800000u) - 1.0f;
-    }
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float z = (p.wsq ? acc[0][s][e] / mx : acc[0][s][e]) + b4[e];
-      float y = p.bn ? z * inv4[e] + sh4[e] : z;
-      if (p.relu) y = fmaxf(y, 0.0f);
-      if (p.keep < 1.0f) y = (y / p.keep) * p3d_dropout_mask(p.keep, u[e]);
-      if (p.res) y += rv[s][e];
-      o[e] = y;
-    }
-    if (YPK) {
-      // whole tile rows (padding rows included) -- the packed buffers hold them
-      *(f32x4*)(p.Y + ((int64_t)((m0 >> 4) + s) * ngN + ct) * 256 + lane * 4) = o;
-    } else if (row < p.M) {
-      if (vec && ((p.ldy & 3) == 0)) {
-        *(f32x4*)(p.Y + (int64_t)row * p.ldy + n0) = o;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n0 + e < p.N) p.Y[(int64_t)row * p.ldy + n0 + e] = o[e];
-      }
-    }
-  }
-}
-
-// =====================================================================================
 // BN-train forward, second half (split form): batch statistics from the row-tile moments,
 // then y = dropout(relu(BN(z))) (+ residual) on the packed layout: one 16x16 tile per
 // 64-lane workgroup, lane l holding row 16rt + (l&15), columns 16ct + 4(l>>4) .. +3, so
@@ -700,8 +612,7 @@ struct BwdArgs {
 
 // RS = 4: one workgroup owns all (<= 64) rows of its 16 columns (BN sums workgroup-local);
 // RS = 1: 16x16 tiles over a (K/16, M/16) grid, BN sums left as row-tile partials (bnpart).
-// The body on tile (bx, by) of a (K/16, gy) grid; k_dgrad runs it on its own grid, k_dgrad_wg
-// beside weight-gradient tiles of the layer above.
+// The body on tile (bx, by) of a (K/16, gy) grid (k_dgrad).
 template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
 __device__ __forceinline__ void p3d_dgrad_body(const BwdArgs& p, int bx, int by, int gy) {
   __shared__ f32x4 red[(WK > 1) ? (WK - 1) * RS * 64 : 1];
@@ -1308,29 +1219,6 @@ __device__ __forceinline__ void p3d_wgrad_multi_body(const WgradMulti& mw) {
 __global__ __launch_bounds__(256, P3D_WG_PER_CU) void k_wgrad_multi(WgradMulti mw) { p3d_wgrad_multi_body<false>(mw); }
 // the gradient-only form, P3D_WG_PER_CU workgroups per CU (see p3d_wgrad_tile)
 __global__ __launch_bounds__(256, P3D_WG_PER_CU) void k_wgrad_grad(WgradMulti mw) { p3d_wgrad_multi_body<true>(mw); }
-
-// A data-gradient launch carrying the weight-gradient (+ fused Adam) tiles of the layer above:
-// blocks [0, gx*gy) are k_dgrad's tiles of this layer, the rest mw's tiles (256 threads: the
-// upper half of those workgroups exits at once).  The tiles of layer l + 1 ride the dgrad
-// launch of layer l: their dZ is final, W(l + 1) was read by the previous launch, and nothing in
-// this launch reads what they update (this layer's dgrad reads W(l) and layer l - 1's gamma,
-// beta); so the single-GPU step's separate k_wgrad_multi launch shrinks to the first two layers.
-template <int RS, int WK, int DEPTH, int NACC, bool APK, int KIND>
-__global__ __launch_bounds__(64 * WK) void k_dgrad_wg(BwdArgs p, WgradMulti mw, int gx, int gy) {
-  const int b = blockIdx.x, nd = gx * gy;
-  if (b < nd) {
-    if (p.remap_gy > 0) {   // (the exchange siblings of a column tile on one XCD, as k_dgrad)
-      int bx, by;
-      p3d_sibling_remap(b, gx, gy, bx, by);
-      p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, bx, by, gy);
-      return;
-    }
-    p3d_dgrad_body<RS, WK, DEPTH, NACC, APK, KIND>(p, b % gx, b / gx, gy);
-    return;
-  }
-  if (threadIdx.x >= 256) return;
-  p3d_wgrad_multi_tile(mw, b - nd);
-}
 
 // =====================================================================================
 // TF1 ApplyAdam fused with the weight re-pack (one launch per optimizer step)

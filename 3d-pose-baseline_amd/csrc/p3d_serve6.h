@@ -1002,8 +1002,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int t = 0; t < RT; ++t)
               acc[cc][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(rb_[d][cc][e], ra_[d][t][e], acc[cc][t], 0, 0, 0);
       };
-      // slot d refilled with k-group g of the operands (ra2, rw2)
+      // slot d refilled with k-group g of the operands (ra2, rw2): exactly kSlotLoads vector loads
+      // (the post's counted wait below depends on that number)
+      constexpr int kSlotLoads = RT + NCM;
       auto refill = [&](int d, const __amdgpu_buffer_rsrc_t& ra2, const __amdgpu_buffer_rsrc_t& rw2, int g) {
+        static_assert(kSlotLoads == RT + NCM, "one load per row tile and one per column tile");
 #pragma unroll
         for (int t = 0; t < RT; ++t) ra_[d][t] = p3d_ld_sc1(ra2, aoff0 + t * rstride + g * 1024);
 #pragma unroll
@@ -1021,8 +1024,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       round(0);
       // the previous block's post (block 0: nothing new -- one post per block): its stores were issued
       // before this round's DEPTH (RT + NCM) refills, so a wait down to that many leaves the refills in
-      // flight (vmcnt retires in issue order) and finds the stores acknowledged
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH * (RT + NCM)) : "memory");
+      // flight (vmcnt retires in issue order) and finds the stores acknowledged.  This holds only while
+      // at least that many vector-memory operations follow the stores in the code the compiler emits:
+      // the "s_nop 5" marks the wait so that tests/test_kernel_resources.py can count them in the
+      // built ISA -- fewer would let the flag overtake the stores
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_nop 5" ::"n"(DEPTH * kSlotLoads) : "memory");
       post_wave();
       __builtin_amdgcn_sched_barrier(0);
       for (int g0 = DEPTH; g0 < gcount - 2 * DEPTH; g0 += DEPTH) round(g0);

@@ -18,6 +18,26 @@ from __future__ import annotations
 import os
 
 
+def free_port(lo=20000, hi=29999):
+    """A free 127.0.0.1 TCP port for a rendezvous, picked at random BELOW the kernel's ephemeral
+    range (32768-60999): a port the OS handed out and we released can go to another socket (RCCL
+    and gloo open many) before the rendezvous binds it -- the EADDRINUSE flake of r05_t20.  The one
+    helper bench.py and the multi-process tests share."""
+    import random
+    import socket
+    for _ in range(64):
+        p = random.randint(lo, hi)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def dist_state():
     """(initialized, rank, world) of the default process group."""
     import torch.distributed as dist

@@ -631,11 +631,14 @@ class LinearModel(object):
 
     def dp_buckets(self, bucket_mb=None, gloo=False):
         """Enable (bucket_mb > 0) or disable (0) the bucketed gradient all-reduce that
-        overlaps the backward (env P3D_DP_BUCKET_MB; default 8 MB on a group of several ranks: at
-        cfg2 two buckets, {output, hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two
-        weight-gradient launches; default 0 on a 1-rank group, whose all-reduce is the identity, so
-        buckets would buy no overlap and cost two launches and a second optimizer pass: 122.9 vs
-        115.3 us per cfg3 step, profiles/r04_dp1_bucket_ab.json);
+        overlaps the backward (env P3D_DP_BUCKET_MB; at cfg2 8 MB gives two buckets, {output,
+        hidden 4, hidden 3} and {hidden 2, hidden 1, input}, i.e. two weight-gradient launches).
+        Default 0 on every group size (round 6): one all-reduce of the flat gradient on
+        the compute stream after the backward, then one optimizer pass.  The bucketed form can hide
+        at most the first bucket's all-reduce under the data gradients that follow it (about 30 us of
+        launches at cfg2), and its comm-stream fork costs every rank about 56 us per step before any
+        byte moves (the N > 1 branch forced on one rank: 169.4 vs 113.4 us, BENCH_r05), so it loses
+        at every collective time;
         RCCL by default, gloo -- host-staged, for tests of several ranks on one GPU -- when
         gloo=True).  Under RCCL the model is attached to the library's own communicator
         (dist_utils.native_comm, p3d_dp_attach) and every DP step is one p3d_train_step_dp.
@@ -644,13 +647,7 @@ class LinearModel(object):
         import ctypes
         import torch.distributed as dist
         if bucket_mb is None:
-            env = os.environ.get("P3D_DP_BUCKET_MB")
-            if env is not None:
-                bucket_mb = float(env)
-            else:
-                multi = (dist.is_initialized() and dist.get_world_size() > 1) or \
-                    os.environ.get("P3D_DP_FORCE_MULTI", "0") not in ("", "0")   # (the N > 1 form on 1 rank)
-                bucket_mb = 8.0 if multi else 0.0
+            bucket_mb = float(os.environ.get("P3D_DP_BUCKET_MB", "0"))
         nccl = self.data_parallel and dist.is_initialized() and dist.get_backend() == "nccl"
         if nccl and getattr(self, "_native", None) is None:
             self._native = dist_utils.attach_native(self)

@@ -52,22 +52,8 @@ def flops_per_pose(L=L, N=NBLK):
 
 
 def _free_port():
-    """A free 127.0.0.1 port below the kernel's ephemeral range (32768-60999): a port the OS handed
-    out and we released can go to another socket (RCCL / gloo open many) before the rendezvous binds
-    it -- the EADDRINUSE flake seen once in the GPU tests (r05_t20)."""
-    import random
-    import socket
-    for _ in range(64):
-        p = random.randint(20000, 29999)
-        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-            try:
-                s.bind(("127.0.0.1", p))
-            except OSError:
-                continue
-        return p
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    import dist_utils
+    return dist_utils.free_port()
 
 
 def launch_ranks(n, dry=False):
@@ -401,6 +387,8 @@ def bench_serve(args, rank, world):
     reps = [round(1e6 * v, 1) for v in samples]     # every timed repeat (value: their median)
     host = {"enqueue_us": med(lambda: run(1)), "launch_sync_us": med(lambda: (run(1), torch.cuda.synchronize())),
             "idle_sync_us": med(torch.cuda.synchronize), "timed_region_repeats_us": reps}
+    if world == 1:
+        host["accounting"] = serve_region_accounting(model, run, R, nrep, world)
     # dominant (only) kernel, timed live: R launches, each carrying a start/stop event pair
     # attached to its dispatch (hipExtLaunchKernel), the interval rocprofv3 reports
     prof = profile_kernels(model, lambda: run(R))
@@ -418,6 +406,57 @@ def bench_serve(args, rank, world):
             "event_pair_avg_us": {k: round(v[1], 3) for k, v in prof.items()}, "host_us": host}
     model.close()
     return value, dt, roof
+
+
+def serve_region_accounting(model, run, R, nrep, world):
+    """Where the headline's timed region goes beyond its kernel, untimed.
+    (a) Paired repeats: the timed region exactly as timed (barrier + synchronize, R launches,
+        barrier + synchronize), each launch carrying its dispatch-attached event pair, so every
+        repeat yields its region time AND its kernel's device time; gap = region - kernel.
+    (b) The same round trip of an EMPTY kernel (256 workgroups, p3d_empty_launch, the same ctypes
+        launch path): its region time and its own device time; overhead = region - device.
+    residual = gap - overhead: what the region pays that a launch + completion of an empty kernel
+    does not (0 if the headline's gap is the launch/completion round trip itself)."""
+    import ctypes
+    import torch
+    import _p3d
+    lib = _p3d.lib()
+    buf = ctypes.create_string_buffer(1 << 12)
+
+    def paired(fn, tag):
+        regions, devs = [], []
+        for _ in range(max(3, nrep)):
+            _p3d.check(lib.p3d_profile_start(model._h, 8), "p3d_profile_start")
+            barrier_sync(world)
+            t0 = time.perf_counter()
+            fn()
+            barrier_sync(world)
+            regions.append(1e6 * (time.perf_counter() - t0))
+            _p3d.check(lib.p3d_profile_stop(model._h, buf, len(buf)), "p3d_profile_stop")
+            tot = 0.0
+            for line in buf.value.decode().strip().splitlines():
+                t, cnt, us = line.split("\t")[:3]
+                if t == tag:
+                    tot += float(us)
+            devs.append(tot)
+        gaps = sorted(r - d for r, d in zip(regions, devs))
+        m = lambda v: sorted(v)[len(v) // 2]   # noqa: E731
+        return {"region_us": round(m(regions), 2), "device_us": round(m(devs), 2), "gap_us": round(gaps[len(gaps) // 2], 2),
+                "regions_us": [round(v, 1) for v in regions], "devices_us": [round(v, 2) for v in devs]}
+
+    empty = lambda: _p3d.check(lib.p3d_empty_launch(model._h, 256, _p3d.stream_handle()), "p3d_empty_launch")  # noqa: E731
+    for _ in range(20):
+        empty()
+    torch.cuda.synchronize()
+    e = paired(empty, "empty")
+    run(3)
+    torch.cuda.synchronize()
+    k = paired(lambda: run(R), "serve")
+    return {"serve_paired": k, "empty_kernel": e,
+            "launch_completion_overhead_us": round(e["gap_us"], 2),
+            "residual_us": round(k["gap_us"] - e["gap_us"], 2),
+            "note": "gap = timed region - the kernel's event-timed device time, per repeat (median); the empty "
+                    "kernel's gap is the launch + completion round trip with no work; residual = serve gap - empty gap"}
 
 
 def bench_latency_b64(reps=300):
@@ -671,25 +710,12 @@ def bench_train(args, rank, world, steps=None, warmup=None, bucket_mb=None, dp=N
         shapes = [(IN, L)] + [(L, L)] * (2 * NBLK) + [(L, OUT)]
         byts = sum(4 * (BATCH * K + BATCH * N) + w_bytes * K * N + 4 * 6 * N for K, N in shapes)
         byts += 4 * 12 * L * (2 * NBLK + 1)          # gamma, beta of every BN layer
-        if "wgrad_side" in prof:
-            # default side form: layer l's dW + Adam (l >= 1) launched on the model's side stream
-            # right after dgrad(l), overlapping the rest of the dgrad chain; layer 0's tiles
-            # (K = 32) ride the step's last launch ("wgrad_tail").  Roofline over the side
-            # launches: bytes of layers 1.. ÷ (launches per step x their average duration).
-            cnt, avg_us, _, _ = prof["wgrad_side"]
-            per_step = len(shapes) - 1
-            K0, N0 = shapes[0]
-            byts = byts - (4 * (BATCH * K0 + BATCH * N0) + w_bytes * K0 * N0 + 4 * 6 * N0)
-            kname = ("k_wgrad_multi on the side stream (fused TF1 Adam + Wf/Wd re-pack), one launch per layer "
-                     "for layers 1..%d, each overlapping the remaining dgrad chain" % per_step)
-            traffic = None
-        else:
-            multi = "wgrad_multi" in prof            # all layers in one launch
-            cnt, avg_us, _, _ = prof["wgrad_multi" if multi else "wgrad"]
-            per_step = 1 if multi else len(shapes)
-            kname = ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
-                     if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step)
-            traffic = _committed_traffic("k_wgrad_multi" if multi else "k_wgrad", {"mode": "train", "batch": BATCH})
+        multi = "wgrad_multi" in prof            # all layers in one launch
+        cnt, avg_us, _, _ = prof["wgrad_multi" if multi else "wgrad"]
+        per_step = 1 if multi else len(shapes)
+        kname = ("k_wgrad_multi (fused TF1 Adam + Wf/Wd re-pack), all %d layers in one launch" % len(shapes)
+                 if multi else "k_wgrad (fused TF1 Adam + Wf/Wd re-pack), all %d layers" % per_step)
+        traffic = _committed_traffic("k_wgrad_multi" if multi else "k_wgrad", {"mode": "train", "batch": BATCH})
         achieved = byts / (per_step * avg_us * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
@@ -1082,11 +1108,10 @@ def cpu_data_baseline(seconds):
 
 def model_bucket_mb(args, world):
     """The gradient-bucket size a DP run uses: --dp-bucket-mb if given, else the library's policy
-    (LinearModel.dp_buckets: 8 MB on several ranks, none on one)."""
+    (LinearModel.dp_buckets: none -- one all-reduce after the backward -- unless P3D_DP_BUCKET_MB)."""
     if args.dp_bucket_mb is not None:
         return args.dp_bucket_mb
-    env = os.environ.get("P3D_DP_BUCKET_MB")
-    return float(env) if env is not None else (8.0 if world > 1 else 0.0)
+    return float(os.environ.get("P3D_DP_BUCKET_MB", "0"))
 
 
 def run_dp1_child(args, timeout=300):
@@ -1135,22 +1160,28 @@ def dp1_child(args, json_fd):
            "value": round(dv, 1), "unit": "poses/s", "mode": dmode,
            "ms_per_step": round(1000.0 * ddt / args.train_steps, 5),
            "event_pair_avg_us": droof.get("event_pair_avg_us")}
-    # the form every rank of an N > 1 run executes (P3D_DP_FORCE_MULTI): 8 MB buckets,
-    # the comm-stream fork, one ncclAllReduce(ncclAvg) per bucket behind its gradient-ready event,
-    # the rev joins, each bucket's Adam on the compute stream -- on this 1-rank group, so what it
-    # times is the form's per-rank cost without any xGMI transfer
+    # the forms a rank of an N > 1 run can execute (P3D_DP_FORCE_MULTI), forced on this
+    # 1-rank group, so what they time is each form's per-rank cost without any xGMI transfer:
+    #   n_gt_1_form (the default): one ncclAllReduce(ncclAvg) of the flat gradient on the compute
+    #     stream after the backward, then one TF1 Adam + re-pack pass;
+    #   n_gt_1_bucketed: 8 MB buckets, the comm-stream fork, one ncclAllReduce(ncclAvg) per bucket
+    #     behind its gradient-ready event, the joins, each bucket's Adam on the compute stream
     if os.environ.get("P3D_DP_FORCE_MULTI") is None:
         os.environ["P3D_DP_FORCE_MULTI"] = "1"
         try:
-            mv, mdt, mroof, mmode = bench_train(args, 0, 1, steps=args.train_steps, warmup=64, dp=True)
-            out["n_gt_1_form"] = {
-                "workload": "the N > 1 data-parallel step forced on the 1-rank group (P3D_DP_FORCE_MULTI=1): "
-                            "%g MB buckets, comm-stream fork, per-bucket ncclAllReduce(ncclAvg) behind the "
-                            "gradient-ready events, joins, per-bucket TF1 Adam on the compute stream, one HIP "
-                            "graph" % (args.dp_bucket_mb if args.dp_bucket_mb is not None else 8.0),
-                "value": round(mv, 1), "unit": "poses/s", "mode": mmode,
-                "ms_per_step": round(1000.0 * mdt / args.train_steps, 5),
-                "event_pair_avg_us": mroof.get("event_pair_avg_us")}
+            for key, bmb in (("n_gt_1_form", 0.0), ("n_gt_1_bucketed", 8.0)):
+                mv, mdt, mroof, mmode = bench_train(args, 0, 1, steps=args.train_steps, warmup=64, dp=True,
+                                                    bucket_mb=bmb)
+                form = ("one ncclAllReduce(ncclAvg) of the flat gradient on the compute stream after the backward, "
+                        "one TF1 Adam + re-pack pass (the default)" if bmb == 0 else
+                        "%g MB buckets, comm-stream fork, per-bucket ncclAllReduce(ncclAvg) behind the gradient-ready "
+                        "events, joins, per-bucket TF1 Adam on the compute stream" % bmb)
+                out[key] = {
+                    "workload": "the N > 1 data-parallel step forced on the 1-rank group (P3D_DP_FORCE_MULTI=1): "
+                                "%s, one HIP graph" % form,
+                    "value": round(mv, 1), "unit": "poses/s", "mode": mmode,
+                    "ms_per_step": round(1000.0 * mdt / args.train_steps, 5),
+                    "event_pair_avg_us": mroof.get("event_pair_avg_us")}
         finally:
             del os.environ["P3D_DP_FORCE_MULTI"]
     dist_utils.close_native_comms()
@@ -1180,7 +1211,7 @@ def build_arg_parser():
     ap.add_argument("--keep", type=float, default=0.5, help="dropout keep_prob of the train step")
     ap.add_argument("--dp-bucket-mb", type=float, default=None,
                     help="data-parallel gradient all-reduce bucket (MB) overlapping the backward; 0 = one all-reduce "
-                         "(default: the library's policy, 8 MB on several ranks, none on a 1-rank group)")
+                         "after the backward (default: the library's policy, P3D_DP_BUCKET_MB or 0)")
     ap.add_argument("--eval-chunk", type=int, default=8192, help="rows per launch in the cfg4 sweep")
     ap.add_argument("--eval-reps", type=int, default=5)
     ap.add_argument("--no-eval", action="store_true", help="skip the cfg4 sweep sub-measurement (infer mode)")
@@ -1255,14 +1286,18 @@ def main():
                 train = {"error": repr(exc)[:300]}
             if dp1 is not None:
                 train["dp_form_1rank"] = dp1
-            if world > 1 and model_bucket_mb(args, world) > 0 and "error" not in train:
-                try:   # the same steps with one all-reduce after the backward (no overlap)
-                    sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=0)
+            if world > 1 and "error" not in train:
+                # the other N > 1 form on the same ranks: 8 MB buckets overlapping the backward when
+                # the run used one all-reduce after it (the default), else that single all-reduce
+                alt = 8.0 if model_bucket_mb(args, world) == 0 else 0.0
+                key = "bucketed_8mb" if alt else "single_allreduce"
+                try:
+                    sv, sdt, _, _ = bench_train(args, rank, world, steps=args.train_steps, warmup=64, bucket_mb=alt)
                     train["dp_bucket_mb"] = model_bucket_mb(args, world)
-                    train["single_allreduce"] = {"value": round(sv, 1), "unit": "poses/s",
-                                                 "ms_per_step": round(1000.0 * sdt / args.train_steps, 5)}
+                    train[key] = {"value": round(sv, 1), "unit": "poses/s",
+                                  "ms_per_step": round(1000.0 * sdt / args.train_steps, 5)}
                 except Exception as exc:
-                    train["single_allreduce"] = {"error": repr(exc)[:300]}
+                    train[key] = {"error": repr(exc)[:300]}
         if not args.no_eval:
             try:
                 sweep = bench_eval(args, rank, world)

@@ -313,6 +313,11 @@ void* p3d_dlpack_alias(void* data, int32_t ndim, const int64_t* shape, int32_t d
 int p3d_profile_start(p3d_model* m, int32_t max_launches);
 int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len);
 
+/* Host-overhead probe (bench.py's accounting of the timed region beyond the kernel): one launch
+ * of an empty kernel of `grid` 256-thread workgroups on `stream`, through the same launch path as
+ * the model's kernels (with the model's event pair while p3d_profile_start is active). */
+int p3d_empty_launch(p3d_model* m, int32_t grid, void* stream);
+
 /* Roofline timing hook: `reps` back-to-back launches of hidden layer `layer`
  * (1 .. 2*num_layers) of the inference forward over workspace rows [0, B). */
 int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream);

@@ -2,7 +2,6 @@
 on the box's one GPU (gloo backend, device tensors staged through the host).  The
 8-GPU RCCL run is the driver's; this checks the DP logic of LinearModel end to end."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -20,25 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port():
-    # a port below the kernel's ephemeral range (32768-60999): a port the OS handed out and we
-    # released can be handed to another socket (RCCL / gloo open many) before the rendezvous binds
-    # it -- the EADDRINUSE flake of r05_t20.  A random pick in 20000-29999, checked free.
-    import random
-    for _ in range(64):
-        p = random.randint(20000, 29999)
-        s = socket.socket()
-        try:
-            s.bind(("127.0.0.1", p))
-        except OSError:
-            continue
-        finally:
-            s.close()
-        return p
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    import dist_utils   # the shared helper (3d-pose-baseline_amd/dist_utils.py)
+    return dist_utils.free_port()
 
 
 def _worker(rank, world, port, out):
@@ -275,7 +257,7 @@ def _check_dp_free_running(r, L, steps, tag="bucketed"):
     arithmetics part ways (TF1 Adam's eps = 1e-8 turns a noise-level gradient difference into a
     sizeable update difference), so the yardstick is the oracle's own float32 restatement: per
     tensor the HIP path's deviation from float64 (L2, relative to how far training moved the
-    tensor; moving statistics relative to their norm) must stay within twice float32's + 1e-3.
+    tensor; moving statistics relative to their norm) must stay within twice float32's + 1e-5.
     Pre-BN biases are excluded (their gradient is analytically zero under BN).
     Returns {tensor: (hip, f32)}."""
     from oracle import ref_mlp
@@ -408,7 +390,7 @@ def test_dp_graph_step_bit_identical_to_eager(tmp_path):
     assert r["graph/step"][0] == 4
 
 
-def _worker_rccl_graph(rank, world, port, out):
+def _worker_rccl_graph(rank, world, port, out, bucket_mb=8):
     sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -428,7 +410,7 @@ def _worker_rccl_graph(rank, world, port, out):
             for i in range(3):
                 m.train_step_device(xs[i], ts[i], 0.5)
         else:
-            m.dp_buckets(8)
+            m.dp_buckets(bucket_mb)
             m.train_step_device(xs[0], ts[0], 0.5)       # eager first step (communicator set up)
             if tag == "eager":
                 for i in (1, 2):
@@ -451,19 +433,22 @@ def _worker_rccl_graph(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("force_multi", ["0", "1"])
-def test_dp_rccl_step_graph_capture(tmp_path, monkeypatch, force_multi):
-    """The RCCL data-parallel step captured in ONE HIP graph (the bucket all-reduces captured on
-    the comm stream, forked from the step by the bucket events and joined before Adam): a 1-rank
-    RCCL group (the box has one GPU), 2 buckets at cfg3's size; the captured step == the eager DP
-    step, and (average of one replica) == the fused single-GPU step, bit for bit.
+@pytest.mark.parametrize("force_multi,bucket_mb", [("0", 8), ("1", 8), ("1", 0)])
+def test_dp_rccl_step_graph_capture(tmp_path, monkeypatch, force_multi, bucket_mb):
+    """The RCCL data-parallel step captured in ONE HIP graph: a 1-rank RCCL group (the box has one
+    GPU) at cfg3's size; the captured step == the eager DP step, and (average of one replica) ==
+    the fused single-GPU step, bit for bit.
+    bucket_mb = 8: 2 buckets, the bucket all-reduces captured on the comm stream, forked from the
+    step by the bucket events and joined before Adam.
     force_multi = 1 (P3D_DP_FORCE_MULTI): the 1-rank group takes p3d_train_step_dp's
-    N > 1 branch -- the comm-stream fork, one ncclAllReduce(ncclAvg) per bucket behind its
-    gradient-ready event, the rev joins, per-bucket Adam on the compute stream -- the code every
-    rank of an 8-GPU run executes, captured and eager, still bit-identical to the fused step."""
+    N > 1 branch, the code every rank of an 8-GPU run executes, captured and eager, still
+    bit-identical to the fused step -- with buckets (the comm-stream fork, one
+    ncclAllReduce(ncclAvg) per bucket behind its gradient-ready event, the rev joins, per-bucket
+    Adam on the compute stream) and without (round 6's default: one ncclAllReduce(ncclAvg) of the
+    flat gradient on the compute stream after the backward, then one optimizer pass)."""
     monkeypatch.setenv("P3D_DP_FORCE_MULTI", force_multi)
     out = str(tmp_path / "r.npz")
-    mp.spawn(_worker_rccl_graph, args=(1, free_port(), out), nprocs=1, join=True)
+    mp.spawn(_worker_rccl_graph, args=(1, free_port(), out, bucket_mb), nprocs=1, join=True)
     r = np.load(out)
     np.testing.assert_array_equal(r["graph"], r["eager"])
     np.testing.assert_array_equal(r["graph"], r["local"])

@@ -11,7 +11,6 @@ recompute inside a GPU test).  Tolerance: north_star's 1e-4 mm on every action a
 unweighted Average.
 """
 import os
-import socket
 import sys
 
 import numpy as np
@@ -69,25 +68,8 @@ def test_cfg4_action_wise_one_rank_vs_oracle(gold):
 
 
 def _free_port():
-    # a port below the kernel's ephemeral range (32768-60999): a port the OS handed out and we
-    # released can be handed to another socket (RCCL / gloo open many) before the rendezvous binds
-    # it -- the EADDRINUSE flake of r05_t20.  A random pick in 20000-29999, checked free.
-    import random
-    for _ in range(64):
-        p = random.randint(20000, 29999)
-        s = socket.socket()
-        try:
-            s.bind(("127.0.0.1", p))
-        except OSError:
-            continue
-        finally:
-            s.close()
-        return p
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    import dist_utils   # the shared helper (3d-pose-baseline_amd/dist_utils.py)
+    return dist_utils.free_port()
 
 
 def _worker(rank, world, port, out):

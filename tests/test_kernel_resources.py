@@ -87,3 +87,36 @@ def test_weight_gradient_kernels_fit_four_per_cu(res, name):
     r = _find(res, name)
     assert r.get("group_segment_fixed_size", 0) <= 40960, (name, r)
     assert r.get("vgpr_count", 0) + r.get("agpr_count", 0) <= 128, (name, r)
+
+
+def test_pair_form_post_wait_follows_its_refills():
+    """k_serve6's pair form posts a block's flag after `s_waitcnt vmcnt(DEPTH (RT +
+    NCM))` -- the previous block's epilogue stores are acknowledged once no more than the round's
+    refill loads are outstanding, which holds only while at least that many vector-memory operations
+    follow the stores in the emitted code (vmcnt retires in issue order).  A compiler change that
+    hoisted a refill above the stores, or dropped one, would let the flag overtake the stores:
+    silent stale reads.  The wait is marked (`s_nop 5`, p3d_serve6.h); walking back from every
+    marked wait to the nearest store or label must cross at least DEPTH (RT + NCM) = 4 (5 + 2) = 28
+    vector loads (a label ends the count early, so the count is a lower bound: a conservative
+    check)."""
+    import re
+    if not os.path.exists(LIB):
+        pytest.skip("libp3d.so not built")
+    from tools.kernel_resources import kernel_isa
+    isa = kernel_isa("void k_serve6<4, 3, 2, 5, true>", LIB)
+    need = 4 * (5 + 2)
+    marks = [i for i in range(len(isa) - 1)
+             if "s_waitcnt vmcnt(%d)" % need in isa[i] and "s_nop 5" in isa[i + 1]]
+    assert marks, "the marked post wait is missing from the pair kernel"
+    vmem = re.compile(r"\s(buffer|global|flat|scratch)_(\w+)")
+    label = re.compile(r"^[0-9a-f]{16} <")
+    for i in marks:
+        loads, j = 0, i - 1
+        while j > 0 and not label.match(isa[j]):
+            m = vmem.search(isa[j])
+            if m and ("store" in m.group(2) or "atomic" in m.group(2)):
+                break
+            if m:
+                loads += 1
+            j -= 1
+        assert loads >= need, (i, loads, isa[j].strip())

@@ -4,6 +4,7 @@ reference's data_utils/procrustes -- tests/golden/make_golden.py), against publi
 Philox4x32-10 known-answer vectors, and cross-checked against torch-CPU autograd for the
 MLP arithmetic that TensorFlow (absent) would compute ("parity unpinned")."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -277,3 +278,18 @@ def test_cfg4_fixture_matches_its_generator():
     assert int(g["frames"].sum()) == 494784
     counts = np.random.default_rng(4).integers(20000, 40001, 15)   # bench.py bench_eval's draw
     assert int(sum(int(c) // 64 for c in counts)) * 64 == 494784
+
+
+@pytest.mark.parametrize("L,N,nnz,B", [(1024, 2, 8, 1280), (4096, 4, 4, 1024), (512, 1, 8, 200)])
+def test_integer_models_are_exact(L, N, nnz, B):
+    """tests/exact_models.py: the integer-valued models the bit-exact GPU tests use really are
+    exact -- every float32 oracle value an integer below 2^23 (exact_forward asserts it), the
+    float64 and float32 accumulations of the bf16 emulation identical -- so 'bit for bit' there is
+    a property of the arithmetic, not of one summation order."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import exact_models
+    cfg, st = exact_models.integer_state(L, N, nnz=nnz)
+    x = exact_models.integer_inputs(B, seed=L + B)
+    out = exact_models.exact_forward(st, x)
+    assert float((out != 0).mean()) > 0.5            # not a degenerate all-zero network
+    assert np.array_equal(ref_mlp.forward_bf16(st, x, acc=np.float64), ref_mlp.forward_bf16(st, x, acc=np.float32))

@@ -56,6 +56,30 @@ def kernel_resources(lib=LIB, arch="gfx950"):
     return {dm: dict(out[n], mangled=n) for n, dm in zip(names, dem)}
 
 
+def kernel_isa(name_prefix, lib=LIB, arch="gfx950"):
+    """Disassembly lines of the first kernel of `lib` whose demangled name starts with
+    `name_prefix` (llvm-objdump of the unbundled gfx950 code object), from its symbol to the next
+    kernel symbol."""
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "co.o")
+        subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, lib, os.devnull],
+                       check=True, capture_output=True)
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + fat,
+                        "--targets=hipv4-amdgcn-amd-amdhsa--" + arch, "--output=" + co], check=True, capture_output=True)
+        dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--symbolize-operands", co], check=True,
+                             capture_output=True, text=True).stdout.split("\n")
+    sym = re.compile(r"^[0-9a-f]{16} <(_Z\w+)>:$")
+    mangled = [(i, m.group(1)) for i, line in enumerate(dis) for m in [sym.match(line)] if m]
+    filt = shutil.which("c++filt") or os.path.join(LLVM, "llvm-cxxfilt")
+    dem = subprocess.run([filt], input="\n".join(n for _, n in mangled), capture_output=True, text=True,
+                         check=True).stdout.splitlines()
+    for k, ((i, _), dm) in enumerate(zip(mangled, dem)):
+        if dm.startswith(name_prefix):
+            end = mangled[k + 1][0] if k + 1 < len(mangled) else len(dis)
+            return dis[i:end]
+    raise KeyError(name_prefix)
+
+
 def main(argv):
     lib = next((a for a in argv if a.endswith(".so")), LIB)
     flt = argv[argv.index("--filter") + 1] if "--filter" in argv else ""
