@@ -1,0 +1,128 @@
+"""Where the drop-in API's host time goes, on the GPU box:
+
+  python tools/api_probe.py
+
+(1) LinearModel.step(isTraining=False) at B = 64 from numpy, as shipped; (2) its pieces; (3) eager
+alternatives: p3d_serve reading x straight from pinned host memory and writing y there (zero-copy),
+p3d_mse on the pinned buffers, one synchronize; the same with device buffers and explicit copies;
+(4) FrameLifter (graph per frame) vs an eager p3d_lift on the pinned buffers.  Prints JSON."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-pose-baseline_amd"))
+sys.path.insert(0, ROOT)
+
+
+def med(fn, n=400, warm=50):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return round(1e6 * ts[len(ts) // 2], 2)
+
+
+def main():
+    import torch
+    import _p3d
+    import bench
+    lib = _p3d.lib()
+    torch.cuda.set_device(0)
+    model, _ = bench.make_model(data_parallel=False, max_batch=64)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((64, 32))
+    t = rng.standard_normal((64, 48))
+    out = {}
+    out["step_eval_b64"] = med(lambda: model.step(None, x, t, 1.0, isTraining=False))
+    st = model._host_step_state(False, 64, 1.0)
+    out["pieces"] = {
+        "copyto_x_t": med(lambda: (np.copyto(st["hx_np"], x, casting="unsafe"), np.copyto(st["ht_np"], t, casting="unsafe"))),
+        "graph_replay_sync": med(lambda: (st["graph"].replay(), torch.cuda.current_stream().synchronize())),
+        "check_errors": med(model.check_errors),
+        "out_copy": med(lambda: st["hy_np"].copy()),
+        "sync_idle": med(lambda: torch.cuda.current_stream().synchronize()),
+    }
+    f32 = torch.float32
+    hx = torch.empty((64, 32), dtype=f32, pin_memory=True)
+    ht = torch.empty((64, 48), dtype=f32, pin_memory=True)
+    hy = torch.empty((64, 48), dtype=f32, pin_memory=True)
+    hl = torch.empty((4,), dtype=f32, pin_memory=True)
+    hx.numpy()[:] = x
+    ht.numpy()[:] = t
+    dx = torch.empty((64, 32), dtype=f32, device="cuda")
+    dt_ = torch.empty((64, 48), dtype=f32, device="cuda")
+    dy = torch.empty((64, 48), dtype=f32, device="cuda")
+    dl = torch.empty((4,), dtype=f32, device="cuda")
+    h = model._h
+    sh = _p3d.stream_handle
+
+    def zc():
+        _p3d.check(lib.p3d_serve(h, hx.data_ptr(), 64, hy.data_ptr(), sh()), "serve")
+        _p3d.check(lib.p3d_mse(hy.data_ptr(), ht.data_ptr(), 64, 48, hl.data_ptr(), 0, sh()), "mse")
+        torch.cuda.current_stream().synchronize()
+
+    def zc_dev_y():
+        _p3d.check(lib.p3d_serve(h, hx.data_ptr(), 64, dy.data_ptr(), sh()), "serve")
+        _p3d.check(lib.p3d_mse(dy.data_ptr(), ht.data_ptr(), 64, 48, hl.data_ptr(), 0, sh()), "mse")
+        hy.copy_(dy, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    def copies():
+        dx.copy_(hx, non_blocking=True)
+        dt_.copy_(ht, non_blocking=True)
+        _p3d.check(lib.p3d_serve(h, dx.data_ptr(), 64, dy.data_ptr(), sh()), "serve")
+        _p3d.check(lib.p3d_mse(dy.data_ptr(), dt_.data_ptr(), 64, 48, dl.data_ptr(), 0, sh()), "mse")
+        hy.copy_(dy, non_blocking=True)
+        hl.copy_(dl, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    def serve_only_zc():
+        _p3d.check(lib.p3d_serve(h, hx.data_ptr(), 64, hy.data_ptr(), sh()), "serve")
+        torch.cuda.current_stream().synchronize()
+
+    def serve_only_dev():
+        _p3d.check(lib.p3d_serve(h, dx.data_ptr(), 64, dy.data_ptr(), sh()), "serve")
+        torch.cuda.current_stream().synchronize()
+
+    ref = model.step(None, x, t, 1.0, isTraining=False)
+    zc()
+    a_zc = hy.numpy().copy()
+    copies()
+    out["eager"] = {"zero_copy_serve_mse": med(zc), "zero_copy_x_dev_y": med(zc_dev_y), "copies_serve_mse": med(copies),
+                    "serve_only_zero_copy": med(serve_only_zc), "serve_only_device": med(serve_only_dev)}
+    out["agree"] = {"zc_vs_copies_bitwise": bool(np.array_equal(a_zc, hy.numpy())),
+                    "zc_vs_step_maxabs": float(np.abs(a_zc - ref[2]).max()),
+                    "loss_zc": float(hl.numpy()[0]), "loss_step": float(ref[0])}
+    # FrameLifter
+    import data_utils
+    import openpose_frontend
+    rng2 = np.random.default_rng(600)
+    use2, _ = data_utils.dimension_sets(2)
+    _, ign3 = data_utils.dimension_sets(3)
+    fl = openpose_frontend.FrameLifter(model, rng2.uniform(200, 600, 64), rng2.uniform(50, 150, 64), use2,
+                                       rng2.uniform(-400, 400, 96), rng2.uniform(30, 300, 96), ign3, batch=1)
+    e = openpose_frontend.map_frames(rng2.uniform(100, 900, (1, 36)))
+    out["frontend_graph"] = med(lambda: fl.lift_mapped(e))
+    r_graph = fl.lift_mapped(e)
+
+    def eager_lift():
+        fl.hin_np[:1] = e
+        openpose_frontend.lift(model, fl.hin, fl.m2, fl.s2, fl.u2, fl.m3, fl.s3, fl.u3, out=fl.hout)
+        torch.cuda.current_stream().synchronize()
+        return fl.hout_np[:1].copy()
+    out["frontend_eager_zero_copy"] = med(eager_lift)
+    out["frontend_agree_bitwise"] = bool(np.array_equal(eager_lift(), r_graph))
+    print(json.dumps(out), flush=True)
+    model.close()
+
+
+if __name__ == "__main__":
+    main()

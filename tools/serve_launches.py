@@ -1,9 +1,13 @@
-"""Durations of every persistent serve launch in a rocprofv3 --kernel-trace CSV of
-`bench.py --gpus 1 --steps 20 --warmup 5` (tools/profile_driver.sh), with bench_serve's launch
-order, next to what the bench measured in the same run.
+"""Durations of the headline's persistent serve launches in a rocprofv3 --kernel-trace CSV of
+`bench.py --gpus 1 --steps 20 --warmup 5` (tools/profile_driver.sh), in bench_serve's launch order,
+next to what the bench measured with its own dispatch-attached events in the same run:
 
     python tools/serve_launches.py <trace dir> <bench_under_rocprof.json> > profiles/rNN_serve_launches.json
-"""
+
+bench_serve's launches of the headline kernel, in order: W warm-up, 100 pre-warm, 3 untimed
+rehearsals of the timed region, the 9 timed repeats, 30 enqueue samples, 30 launch + synchronize
+samples, 3 settling launches, the 9 paired repeats of the region accounting (each with its event
+pair: the line's roofline avg_us is their median), 1 more event-timed launch."""
 import csv
 import glob
 import json
@@ -11,25 +15,36 @@ import os
 import sys
 
 
+def med(v):
+    v = sorted(v)
+    return v[len(v) // 2] if v else None
+
+
 def main():
     tdir, bench = sys.argv[1], sys.argv[2]
+    line = json.loads([ln for ln in open(bench) if ln.startswith("{")][-1])
+    roof = line["roofline"]
+    kname = roof["kernel"].split(" (")[0]
     f = glob.glob(os.path.join(tdir, "*kernel_trace.csv"))[0]
-    rows = [r for r in csv.DictReader(open(f)) if "k_serve" in r["Kernel_Name"] and "prep" not in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("void " + kname[:-1])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    names = sorted({r["Kernel_Name"] for r in rows})
     dur = [round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0, 3) for r in rows]
-    line = json.loads(open(bench).read().strip().splitlines()[-1])
-    wl = line["roofline"]["warmup_launches"]
-    timed = wl + 100 + 3                       # bench_serve: warm-up, pre-warm, 3 rehearsals, then the timed launch
-    out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20 --warmup 5",
-           "kernel": names, "launches": len(dur),
-           "order": "bench_serve: %d warm-up + 100 pre-warm + 3 untimed rehearsal launches, #%d the timed one, "
-                    "then 8 repeats of the timed region, 30 + 30 host-overhead samples, the last the "
-                    "event-timed (roofline) launch" % (wl, timed + 1),
-           "timed_launch_us": dur[timed] if timed < len(dur) else None,
-           "event_timed_launch_us": dur[-1],
-           "median_after_prewarm_us": sorted(dur[wl + 100:])[len(dur[wl + 100:]) // 2],
-           "bench_value_same_run": line["value"], "bench_event_avg_us_same_run": line["roofline"]["avg_us"],
+    wl = roof["warmup_launches"]
+    i_timed = wl + 100 + 3
+    i_paired = i_timed + 9 + 30 + 30 + 3
+    acc = roof["host_us"].get("accounting", {}).get("serve_paired", {})
+    timed, paired = dur[i_timed:i_timed + 9], dur[i_paired:i_paired + 9]
+    out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-dp1",
+           "kernel": sorted({r["Kernel_Name"] for r in rows}), "launches": len(dur),
+           "timed_repeats_us": timed, "timed_repeats_median_us": med(timed),
+           "paired_repeats_us": paired, "paired_repeats_median_us": med(paired),
+           "bench_paired_event_us_same_run": acc.get("devices_us"),
+           "bench_paired_event_median_us_same_run": acc.get("device_us"),
+           "bench_roofline_avg_us_same_run": roof["avg_us"],
+           "last_launch_us": dur[-1] if dur else None,
+           "all_launches_avg_us": round(sum(dur) / len(dur), 3) if dur else None,
+           "median_after_prewarm_us": med(dur[wl + 100:]),
+           "bench_value_same_run": line["value"],
            "durations_us": dur}
     print(json.dumps(out, indent=1))
 
