@@ -18,6 +18,7 @@ P3D_CTR_GLOBAL_STEP = 0xFFFFFFFFFFFFFFFF
 P3D_DTYPE_F32 = 0
 P3D_DTYPE_BF16 = 1
 P3D_DTYPE_F64 = 2
+P3D_ERR_ARG = 1          # include/p3d.h status codes (check() maps 1 to ValueError)
 
 
 class P3DCfg(ctypes.Structure):
@@ -49,6 +50,7 @@ SIGNATURES = [
     ("p3d_forward_ex", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_float, c_uint64,
                                  c_uint64, c_int64, c_int64, c_void_p]),
     ("p3d_serve", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("p3d_serve_mse", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("p3d_serve_check", c_int32, [c_void_p]),
     ("p3d_sync_check", c_int32, [c_void_p]),
     ("p3d_error_flags", c_int32, [c_void_p, POINTER(c_int32), c_int32]),

@@ -190,6 +190,7 @@ struct p3d_model {
   // census/barrier words and the spin-timeout flag; allocated at the first call
   float* serve_buf = nullptr;
   float* serve6_act = nullptr;   // k_serve6's activation slabs (4 per group, P3D_SERVE6_ROWS rows in all)
+  float* serve_loss = nullptr;   // p3d_serve_mse: per-output-tile partials + the arrival counter
   float* serve_ecg = nullptr;      // k_serve6 epilogue-constant table (k_serve_prep), [layer][tile][48] + divisors
   bool serve_ec_dirty = true;      // parameters or moving statistics changed since the table was formed
   unsigned* serve_sync = nullptr;  // [k_serve6 bank 0 | bank 1 | k_serve5 bank | device epoch word ...]
@@ -292,6 +293,7 @@ void free_all(p3d_model* m) {
   if (m->abf) (void)hipFree(m->abf);
   if (m->serve_buf) (void)hipFree(m->serve_buf);
   if (m->serve6_act) (void)hipFree(m->serve6_act);
+  if (m->serve_loss) (void)hipFree(m->serve_loss);
   if (m->serve_sync) (void)hipFree(m->serve_sync);
   if (m->serve_ecg) (void)hipFree(m->serve_ecg);
   if (m->xsync) (void)hipFree(m->xsync);
@@ -1343,7 +1345,8 @@ static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int 
   }
 }
 
-extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream) {
+static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss,
+                      void* stream) {
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_serve: null argument");
   const p3d_cfg& c = m->cfg;
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_serve: batch must be positive");
@@ -1388,6 +1391,12 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
     // is not allowed
     const int64_t n6 = (int64_t)4 * P3D_SERVE6_ROWS * L;
     if ((e = hipMalloc(&m->serve6_act, n6 * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    // the fused MSE's per-tile partials (one per 16-row x 16-column output tile of P3D_SERVE6_ROWS
+    // rows) and its arrival counter (last word), zero between launches
+    if ((e = hipMalloc(&m->serve_loss, (P3D_SERVE6_ROWS / 16 * 4 + 64) * sizeof(float))) != hipSuccess)
+      return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
+    if ((e = hipMemset(m->serve_loss, 0, (P3D_SERVE6_ROWS / 16 * 4 + 64) * sizeof(float))) != hipSuccess)
       return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
     m->serve_ec_dirty = true;
   }
@@ -1449,6 +1458,13 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   }
   // (k_serve6 picks its bank from the device epoch word: no memset in front, graph replays
   // alternate the banks by themselves)
+  if (t && !use6)
+    return fail(P3D_ERR_ARG, "p3d_serve_mse: no k_serve6 form covers this launch (more than 32 batch-64 steps, "
+                             "or a model shape k_serve6 is not built for): use p3d_serve + p3d_mse");
+  if (t) {
+    a.tgt = t; a.loss = loss;
+    a.lpart = m->serve_loss; a.lcnt = (unsigned*)(m->serve_loss + P3D_SERVE6_ROWS / 16 * 4);
+  }
   if (use6) {
     a.act = m->serve6_act;                   // [group][4 slabs][16 RT rows][L]; no output partials
     a.part = nullptr;
@@ -1475,6 +1491,17 @@ extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void
   return P3D_OK;
 }
 
+extern "C" int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream) {
+  return serve_impl(m, x, B, y, nullptr, nullptr, stream);
+}
+
+// (include/p3d.h) p3d_serve with the MSE of linear_model.py:129 fused into its output phase
+extern "C" int p3d_serve_mse(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss,
+                             void* stream) {
+  if (!t || !loss) return fail(P3D_ERR_ARG, "p3d_serve_mse: null argument");
+  return serve_impl(m, x, B, y, t, loss, stream);
+}
+
 static const char* serve_err_text(int v) {
   return v == 2 ? "p3d_serve: an XCD group had fewer workgroups than the launch was sized for"
                 : "p3d_serve: a workgroup's synchronisation timed out (not all workgroups resident); the "
@@ -1485,6 +1512,8 @@ static const char* serve_err_text(int v) {
 static int serve_report(p3d_model* m, int v) {
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess && m->serve_sync) e = hipMemset(m->serve_sync, 0, P3D_SERVE_SYNC_ALL * sizeof(unsigned));
+  // (a failed launch may have left the fused MSE's arrival counter short)
+  if (e == hipSuccess && m->serve_loss) e = hipMemset(m->serve_loss, 0, (P3D_SERVE6_ROWS / 16 * 4 + 64) * sizeof(float));
   if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string("p3d_serve_check: ") + hipGetErrorString(e));
   __atomic_store_n(&m->errw[1], 0, __ATOMIC_SEQ_CST);
   return fail(P3D_ERR_HIP, serve_err_text(v));

@@ -120,6 +120,13 @@ struct ServeArgs {
   int max_groups;      // steps are dealt over at most this many XCD groups (others idle)
   int split;           // k_serve6: groups per XCD (1..4)
   const float* ecg;    // k_serve6: epilogue constants per layer and 16-column tile (k_serve_prep)
+  // fused MSE (p3d_serve_mse, k_serve6 only; tgt == nullptr: off): targets [M, ND] row-major, one
+  // squared-error partial per output tile (lpart), an arrival counter (lcnt, zero between launches)
+  // and the loss word mean((y - t)^2) the last arriving tile writes (src/linear_model.py:129)
+  const float* tgt;
+  float* lpart;
+  unsigned* lcnt;
+  float* loss;
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 
@@ -373,17 +380,56 @@ __device__ __forceinline__ void p3d_serve_partial(const f32x4 (&wo)[NDT], f32x4 
 // This workgroup handles its share [r/n, (r+1)/n) of the float4 elements.
 // y[row, col] = sum / maxnorm + b4 for partial element e4 of the step at row0
 template <int NDT>
-__device__ __forceinline__ void p3d_serve_store_out(const ServeArgs& p, const ServeLayer& lo, f32x4 sum, int e4,
-                                                    int64_t row0) {
+// Stores this lane's 4 outputs; returns their squared error against p.tgt (0 without targets).
+__device__ __forceinline__ float p3d_serve_store_out(const ServeArgs& p, const ServeLayer& lo, f32x4 sum, int e4,
+                                                     int64_t row0) {
   const int tile = e4 >> 6, ln = e4 & 63, rt = tile / NDT, o = tile % NDT;
   const int col = 16 * o + (ln & 15), q = ln >> 4;
-  if (col >= p.ND) return;
+  if (col >= p.ND) return 0.0f;
   const float mx = lo.wsq ? fmaxf(sqrtf(*lo.wsq), 1.0f) : 1.0f;
   const float bb = lo.bias[col];
+  float se = 0.0f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t row = row0 + 16 * rt + 4 * q + k;
-    if (row < p.M) p.y[row * p.ND + col] = (lo.wsq ? sum[k] / mx : sum[k]) + bb;
+    if (row < p.M) {
+      const float yv = (lo.wsq ? sum[k] / mx : sum[k]) + bb;
+      p.y[row * p.ND + col] = yv;
+      if (p.tgt) {
+        const float d = yv - p.tgt[row * p.ND + col];
+        se = __builtin_fmaf(d, d, se);
+      }
+    }
+  }
+  return se;
+}
+
+// Fused MSE, one output tile's share (a whole wave; wave-uniform call): the lanes' squared errors
+// summed in a fixed butterfly, stored as tile gtile's partial (write-through), then one arrival on
+// the launch's counter.  The wave whose arrival is the last sums every tile's partial in a fixed
+// order (lane l: tiles l, l + 64, ...; then the same butterfly) and writes mean = sum / (M ND); it
+// resets the counter for the next launch (stream-ordered behind this one).  Same bits for the same
+// launch shape; tiles past the last row (a pair unit past the end) do not arrive.
+__device__ __forceinline__ void p3d_serve_loss_tile(const ServeArgs& p, float se, int64_t gtile, int64_t ntiles) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) se += __shfl_xor(se, o, 64);
+  if (gtile >= ntiles) return;
+  unsigned v = 0;
+  if (lane == 0) {
+    __hip_atomic_store(p.lpart + gtile, se, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v = __hip_atomic_fetch_add(p.lcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  v = __shfl(v, 0, 64);
+  if ((int64_t)v + 1 != ntiles) return;
+  float t = 0.0f;
+  for (int64_t i = lane; i < ntiles; i += 64) t += __hip_atomic_load(p.lpart + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+  if (lane == 0) {
+    *p.loss = t / (float)(p.M * p.ND);
+    __hip_atomic_store(p.lcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -406,7 +452,7 @@ __device__ __forceinline__ void p3d_serve_reduce(const ServeArgs& p, const Serve
       for (int u = ub + 1; u < ue; ++u) ss += p3d_ld_sc1(rs, (u * E4 + e4) * 16);
       sum += ss;
     }
-    p3d_serve_store_out<NDT>(p, lo, sum, e4, row0);
+    (void)p3d_serve_store_out<NDT>(p, lo, sum, e4, row0);
   }
 }
 
@@ -951,7 +997,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int sl = 0; sl < 4; ++sl) tot += rsum[sl * 64 * RE + tid];
-          p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
+          (void)p3d_serve_store_out<NDT>(p, lo, tot, es + tid, prev_row0);
         }
         f32x4 yv[NC];
 #pragma unroll

@@ -608,8 +608,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int k = 1; k < 4; ++k) tot += sl[k];
         if (broken) tot = f32x4{qnan, qnan, qnan, qnan};
-        if (PAIR && c0 + w >= OT) p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w - OT) * 64 + lane, orow1);
-        else p3d_serve_store_out<NDT>(p, lo, tot, (c0 + w) * 64 + lane, orow0);
+        const bool tb = PAIR && c0 + w >= OT;
+        const int tile = tb ? c0 + w - OT : c0 + w;
+        const int64_t orow = tb ? orow1 : orow0;
+        const float se = p3d_serve_store_out<NDT>(p, lo, tot, tile * 64 + lane, orow);
+        if (p.tgt)                             // fused MSE (p3d_serve_mse): this tile's share
+          p3d_serve_loss_tile(p, se, (orow >> 4) * NDT + tile, ((p.M + 15) >> 4) * NDT);
       }
       if (c0 == o_lo) P3D_S6_OSTAMP(2);
       __syncthreads();                         // red is rewritten next (next round / phase)

@@ -264,6 +264,7 @@ class LinearModel(object):
         self._loss_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._step_host = 0   # host mirror of the device global_step (step() summaries, no sync)
         self._host_steps = {}  # step() staging buffers / eval graphs per (mode, B, keep)
+        self._serve_steps = {}  # step(isTraining=False) one-launch states per batch (p3d_serve_mse)
         self._dy = torch.empty((self.max_batch, self.output_size), dtype=torch.float32, device=self.device)
         if init:
             self.initialize(self.seed)
@@ -832,6 +833,41 @@ class LinearModel(object):
         self._host_steps[key] = st
         return st
 
+    def _serve_step_state(self, B):
+        """Pinned buffers of the one-launch evaluation step (p3d_serve_mse): [x | t] in, y out and
+        the loss word, all read and written by the kernel directly (mapped host memory), with the
+        launch's ctypes arguments bound once.  None when no k_serve6 form covers B (the library
+        says so once: P3D_ERR_ARG) -- the cached-graph path runs then."""
+        st = self._serve_steps.get(B, False)
+        if st is not False:
+            return st
+        torch = self.torch
+        st = None
+        if (not self.bf16 and 4 < B <= 32 * 64 and self.linear_size % 128 == 0 and self.num_layers > 0
+                and os.environ.get("P3D_STEP_SERVE", "1") != "0"):
+            import ctypes
+            f32 = torch.float32
+            nx, nt = B * self.input_size, B * self.output_size
+            hin = torch.empty(nx + nt, dtype=f32, pin_memory=True)
+            hout = torch.empty(nt + 4, dtype=f32, pin_memory=True)
+            st = {"hin": hin, "hout": hout,
+                  "hx_np": hin[:nx].view(B, self.input_size).numpy(), "ht_np": hin[nx:].view(B, self.output_size).numpy(),
+                  "hy_np": hout[:nt].view(B, self.output_size).numpy(), "hl_np": hout[nt:nt + 1].numpy()}
+            args = (self._h, ctypes.c_void_p(hin.data_ptr()), B, ctypes.c_void_p(hout.data_ptr()),
+                    ctypes.c_void_p(hin.data_ptr() + 4 * nx), ctypes.c_void_p(hout.data_ptr() + 4 * nt))
+            fn, sh = lib().p3d_serve_mse, _p3d.stream_handle
+            st["launch"] = lambda: fn(*args, ctypes.c_void_p(sh()))   # noqa: E731
+            np.copyto(st["hx_np"], 0.0)
+            np.copyto(st["ht_np"], 0.0)
+            rc = st["launch"]()
+            torch.cuda.current_stream(self.device).synchronize()
+            if rc == _p3d.P3D_ERR_ARG:
+                st = None                     # no k_serve6 form for this batch: the graph path
+            else:
+                check(rc, "p3d_serve_mse")
+        self._serve_steps[B] = st
+        return st
+
     def _step_host_arrays(self, encoder_inputs, decoder_outputs, keep, training):
         x = np.asarray(encoder_inputs)
         t = np.asarray(decoder_outputs)
@@ -844,6 +880,21 @@ class LinearModel(object):
         B = x.shape[0]
         if B > self.max_batch:
             raise ValueError("batch %d exceeds max_batch %d" % (B, self.max_batch))
+        if not training and keep == 1.0:
+            # evaluation (the reference's evaluate_batches feeds keep 1.0): ONE persistent launch
+            # reading x and t straight from pinned host memory and writing y and the fused MSE
+            # there (p3d_serve_mse) -- no copy nodes, no graph replay
+            ss = self._serve_step_state(B)
+            if ss is not None:
+                np.copyto(ss["hx_np"], x, casting="unsafe")
+                np.copyto(ss["ht_np"], t, casting="unsafe")
+                rc = ss["launch"]()
+                if rc:
+                    check(rc, "p3d_serve_mse")
+                self.torch.cuda.current_stream(self.device).synchronize()
+                self.check_errors()
+                lv = float(ss["hl_np"][0])
+                return lv, Summary("loss/loss", lv), ss["hy_np"].copy()
         st = self._host_step_state(training, B, keep)
         np.copyto(st["hx_np"], x, casting="unsafe")     # float64 -> float32, as the placeholders cast
         np.copyto(st["ht_np"], t, casting="unsafe")

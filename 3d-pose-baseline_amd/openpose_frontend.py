@@ -14,6 +14,8 @@ axis swap and Maya export that follow in the sandbox are out of scope.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import data_pipeline as dp
@@ -50,7 +52,8 @@ def lift(model, raw, mean2, std2, use2, mean3, std3, use3, out):
 
 
 class FrameLifter:
-    """Lift mapped OpenPose frames to 3D (mm) with a LinearModel, one HIP graph per call."""
+    """Lift mapped OpenPose frames to 3D (mm) with a LinearModel: one p3d_lift launch per call on
+    pinned host rows (fp32 models; bf16 models: one HIP graph of the three calls per call)."""
 
     def __init__(self, model, data_mean_2d, data_std_2d, dim_to_use_2d, data_mean_3d, data_std_3d,
                  dim_to_ignore_3d, batch=1):
@@ -77,14 +80,30 @@ class FrameLifter:
             self.y = torch.empty((self.B, model.output_size), dtype=f32, device=dev)
             self.p3 = torch.empty((self.B, D3), dtype=f64, device=dev)
             self.hin.zero_()
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(side):
-                self._body()                           # eager warm-up (no side effects)
-            torch.cuda.current_stream(dev).wait_stream(side)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, stream=side):
-                self._body()
+            self.graph, self._launch = None, None
+            if not model.bf16 and os.environ.get("P3D_LIFT_EAGER", "1") != "0":
+                # fp32 (round 6): ONE p3d_lift launch per call that reads the pinned frame rows and
+                # writes the pinned millimetre rows itself (mapped host memory), its ctypes
+                # arguments bound once -- a graph replay costs more than the launch it would save
+                import ctypes
+                import _p3d
+                c = ctypes.c_void_p
+                args = (model._h, c(self.hin.data_ptr()), self.B, 64, c(self.m2.data_ptr()), c(self.s2.data_ptr()),
+                        c(self.u2.data_ptr()), self.u2.numel(), c(self.m3.data_ptr()), c(self.s3.data_ptr()),
+                        c(self.u3.data_ptr()), self.u3.numel(), D3, c(self.hout.data_ptr()))
+                fn, sh = _p3d.lib().p3d_lift, _p3d.stream_handle
+                self._launch = lambda: fn(*args, c(sh()))   # noqa: E731
+                _p3d.check(self._launch(), "p3d_lift")
+                torch.cuda.current_stream(dev).synchronize()
+            else:
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    self._body()                           # eager warm-up (no side effects)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, stream=side):
+                    self._body()
         self.hin_np, self.hout_np = self.hin.numpy(), self.hout.numpy()
 
     def _body(self):
@@ -107,7 +126,13 @@ class FrameLifter:
         self.hin_np[:n] = e
         if n < self.B:
             self.hin_np[n:] = 0.0
-        self.graph.replay()
+        if self._launch is not None:
+            rc = self._launch()
+            if rc:
+                import _p3d
+                _p3d.check(rc, "p3d_lift")
+        else:
+            self.graph.replay()
         self.torch.cuda.current_stream(self.model.device).synchronize()
         return self.hout_np[:n].copy()
 

@@ -372,10 +372,12 @@ def bench_serve(args, rank, world):
     # serve_check's device read runs on another queue; one more launch + synchronize puts the
     # compute queue back in the state every timed launch starts from (the first launch after
     # the read measured ~25 us slower than the median launch + synchronize round trip)
-    # ~100 launches (~15 ms) of pre-warm: the chip's clock ramps under this load -- launch
-    # durations fall from ~152 to ~136 us over the first ~80 launches
-    # (profiles/r02_v1_serve_launches.json); with 20 the timed launch ran at ~146 us
-    run(int(os.environ.get("P3D_BENCH_PREWARM", "100")))
+    # pre-warm: the chip's clock keeps ramping under this load for ~200 launches (~25 ms): in the
+    # round-6 rocprof trace of this command the launches ran 123 us (#30), 107 (#90), 105 (#110,
+    # where the timed region then sat), 102.5 (#140), 99-100 (#175-190)
+    # (profiles/r06_v1_serve_launches.json); 400 launches (~45 ms) put the timed region on the plateau
+    prewarm = int(os.environ.get("P3D_BENCH_PREWARM", "400"))
+    run(prewarm)
     # and the timed region's own code, untimed (the first pass through it measured ~10 us
     # slower than every later one: host-side first-use costs, not GPU work)
     for _ in range(3):
@@ -427,7 +429,8 @@ def bench_serve(args, rank, world):
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "kernel": kname + " (persistent: %d batch-64 steps per launch, whole network per XCD, fp32 MFMA 16x16x4)" % C,
-            "flop_per_launch": int(flop), "steps_per_launch": C, "warmup_launches": wl, "avg_us": round(avg_us, 3),
+            "flop_per_launch": int(flop), "steps_per_launch": C, "warmup_launches": wl, "prewarm_launches": prewarm,
+            "avg_us": round(avg_us, 3),
             "avg_us_from": "median of the event-timed launches of the 9 paired timed-region repeats" if paired else
                            "one event-timed launch",
             "launches_timed": cnt, "single_launch_event_us": round(prof["serve"][1], 3),

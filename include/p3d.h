@@ -134,6 +134,13 @@ int p3d_forward_ex(p3d_model* m, const float* x, int64_t B, float* y, int32_t tr
  * (other kernels merely delay it).  A launch whose workgroups could not all synchronise
  * stops within ~0.5 s and is reported by the next p3d_serve_check (P3D_ERR_HIP). */
 int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
+/* p3d_serve with the evaluation loss of src/linear_model.py:129 (the `loss` output of the eval
+ * step(), :239-245) fused into the launch: *loss = mean((y - t)^2) over B x output_size, t [B,
+ * output_size] row-major.  x, y, t and loss may be pinned (mapped) host memory: the kernel reads
+ * and writes them directly, so LinearModel.step(isTraining=False) is ONE launch from numpy.
+ * P3D_ERR_ARG where no k_serve6 form covers the launch (> 32 batch-64 steps, or a model shape
+ * it is not built for): the caller uses p3d_serve + p3d_mse there. */
+int p3d_serve_mse(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss, void* stream);
 /* 0 if every p3d_serve launch so far completed its synchronisation (synchronises the device,
  * then reads the kernels' pinned error word).  After a failure p3d_serve refuses new launches
  * (P3D_ERR_HIP) until this call reports it once; the failed launch's rows hold NaN, never

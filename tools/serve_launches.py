@@ -4,7 +4,7 @@ next to what the bench measured with its own dispatch-attached events in the sam
 
     python tools/serve_launches.py <trace dir> <bench_under_rocprof.json> > profiles/rNN_serve_launches.json
 
-bench_serve's launches of the headline kernel, in order: W warm-up, 100 pre-warm, 3 untimed
+bench_serve's launches of the headline kernel, in order: W warm-up, P pre-warm (prewarm_launches), 3 untimed
 rehearsals of the timed region, the 9 timed repeats, 30 enqueue samples, 30 launch + synchronize
 samples, 3 settling launches, the 9 paired repeats of the region accounting (each with its event
 pair: the line's roofline avg_us is their median), 1 more event-timed launch."""
@@ -30,7 +30,7 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0, 3) for r in rows]
     wl = roof["warmup_launches"]
-    i_timed = wl + 100 + 3
+    i_timed = wl + roof.get("prewarm_launches", 100) + 3
     i_paired = i_timed + 9 + 30 + 30 + 3
     acc = roof["host_us"].get("accounting", {}).get("serve_paired", {})
     timed, paired = dur[i_timed:i_timed + 9], dur[i_paired:i_paired + 9]
@@ -43,7 +43,7 @@ def main():
            "bench_roofline_avg_us_same_run": roof["avg_us"],
            "last_launch_us": dur[-1] if dur else None,
            "all_launches_avg_us": round(sum(dur) / len(dur), 3) if dur else None,
-           "median_after_prewarm_us": med(dur[wl + 100:]),
+           "median_after_prewarm_us": med(dur[wl + roof.get("prewarm_launches", 100):]),
            "bench_value_same_run": line["value"],
            "durations_us": dur}
     print(json.dumps(out, indent=1))
