@@ -380,9 +380,11 @@ __device__ __forceinline__ void p3d_serve_partial(const f32x4 (&wo)[NDT], f32x4 
 // This workgroup handles its share [r/n, (r+1)/n) of the float4 elements.
 // y[row, col] = sum / maxnorm + b4 for partial element e4 of the step at row0
 template <int NDT>
-// Stores this lane's 4 outputs; returns their squared error against p.tgt (0 without targets).
+// Stores this lane's 4 outputs; returns their squared error against the lane's 4 targets tv
+// (p3d_serve_load_tgt, requested ahead of the tile's contraction: they may live in host memory) --
+// 0 without targets.
 __device__ __forceinline__ float p3d_serve_store_out(const ServeArgs& p, const ServeLayer& lo, f32x4 sum, int e4,
-                                                     int64_t row0) {
+                                                     int64_t row0, f32x4 tv = f32x4{0.f, 0.f, 0.f, 0.f}) {
   const int tile = e4 >> 6, ln = e4 & 63, rt = tile / NDT, o = tile % NDT;
   const int col = 16 * o + (ln & 15), q = ln >> 4;
   if (col >= p.ND) return 0.0f;
@@ -395,13 +397,25 @@ __device__ __forceinline__ float p3d_serve_store_out(const ServeArgs& p, const S
     if (row < p.M) {
       const float yv = (lo.wsq ? sum[k] / mx : sum[k]) + bb;
       p.y[row * p.ND + col] = yv;
-      if (p.tgt) {
-        const float d = yv - p.tgt[row * p.ND + col];
-        se = __builtin_fmaf(d, d, se);
-      }
+      const float d = yv - tv[k];
+      se = __builtin_fmaf(d, d, se);
     }
   }
-  return se;
+  return p.tgt ? se : 0.0f;
+}
+// The targets of this lane's 4 outputs of output element e4 (rows past the end / columns past
+// output_size: 0, unused)
+template <int NDT>
+__device__ __forceinline__ f32x4 p3d_serve_load_tgt(const ServeArgs& p, int e4, int64_t row0) {
+  const int tile = e4 >> 6, ln = e4 & 63, rt = tile / NDT, o = tile % NDT;
+  const int col = 16 * o + (ln & 15), q = ln >> 4;
+  f32x4 tv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = row0 + 16 * rt + 4 * q + k;
+    if (col < p.ND && row < p.M) tv[k] = p.tgt[row * p.ND + col];
+  }
+  return tv;
 }
 
 // Fused MSE, one output tile's share (a whole wave; wave-uniform call): the lanes' squared errors

@@ -550,6 +550,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const __amdgpu_buffer_rsrc_t ryB = p3d_rsrc(act + (PAIR ? 7 : 3) * slab);
     for (int c0 = o_lo; c0 < o_hi; c0 += OCH) {
       const int nt = min(OCH, o_hi - c0);
+      // fused MSE (p3d_serve_mse): wave w's tile's targets requested before the contraction (they
+      // may be in host memory: a PCIe round trip hidden under the tile's ~2 us of work)
+      f32x4 tv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (p.tgt && w < nt) {
+        const bool tb = PAIR && c0 + w >= OT;
+        tv = p3d_serve_load_tgt<NDT>(p, (tb ? c0 + w - OT : c0 + w) * 64 + lane, tb ? orow1 : orow0);
+      }
       f32x4 oacc[OCH];
 #pragma unroll
       for (int j = 0; j < OCH; ++j) oacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -611,7 +618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const bool tb = PAIR && c0 + w >= OT;
         const int tile = tb ? c0 + w - OT : c0 + w;
         const int64_t orow = tb ? orow1 : orow0;
-        const float se = p3d_serve_store_out<NDT>(p, lo, tot, tile * 64 + lane, orow);
+        const float se = p3d_serve_store_out<NDT>(p, lo, tot, tile * 64 + lane, orow, tv);
         if (p.tgt)                             // fused MSE (p3d_serve_mse): this tile's share
           p3d_serve_loss_tile(p, se, (orow >> 4) * NDT + tile, ((p.M + 15) >> 4) * NDT);
       }

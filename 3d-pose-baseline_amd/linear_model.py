@@ -750,6 +750,10 @@ class LinearModel(object):
         Inputs are numpy arrays (float64 is cast to float32 like the placeholders).
         """
         torch = self.torch
+        if type(encoder_inputs) is np.ndarray and type(decoder_outputs) is np.ndarray and \
+                torch.cuda.current_device() == self.device.index:
+            # (the common call from numpy on the model's device: no device-context switch)
+            return self._step_host_arrays(encoder_inputs, decoder_outputs, float(dropout_keep_prob), bool(isTraining))
         with torch.cuda.device(self.device):
             if not isinstance(encoder_inputs, torch.Tensor) and not isinstance(decoder_outputs, torch.Tensor):
                 return self._step_host_arrays(encoder_inputs, decoder_outputs, float(dropout_keep_prob),

@@ -92,6 +92,13 @@ def main():
         _p3d.check(lib.p3d_serve(h, dx.data_ptr(), 64, dy.data_ptr(), sh()), "serve")
         torch.cuda.current_stream().synchronize()
 
+    ss = model._serve_step_state(64)
+    if ss is not None:
+        np.copyto(ss["hx_np"], x, casting="unsafe")
+        np.copyto(ss["ht_np"], t, casting="unsafe")
+        out["serve_mse_launch_sync"] = med(lambda: (ss["launch"](), torch.cuda.current_stream().synchronize()))
+    out["device_ctx"] = med(lambda: torch.cuda.device(model.device).__enter__())
+    out["current_stream_sync_call"] = med(lambda: torch.cuda.current_stream(model.device).synchronize())
     ref = model.step(None, x, t, 1.0, isTraining=False)
     zc()
     a_zc = hy.numpy().copy()
