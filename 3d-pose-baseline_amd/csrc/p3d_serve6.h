@@ -921,20 +921,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // first build waited for everything in flight before every contraction and every store).
   for (int b = gi; b < p.nb; b += 2 * ng) {
     const int64_t rowA = (int64_t)b * ROWS, rowB = (int64_t)(b + ng) * ROWS;
-    // input layers: both units' operands requested at once, A's computed, B's, one post for both
-    // (the first: binds the bank); block 0's first post then carries nothing new (the count stays
-    // one post per block)
+    // input layers: both units' operands requested at once; A's computed and posted (the first post
+    // binds the bank), then B's computed while A's producers' posts arrive -- B's input layer is
+    // posted by block 0's in-contraction post (its stores precede block 0's ring requests, so that
+    // post's counted wait finds them acknowledged), which block 1 (B's first hidden phase) waits for.
+    // (Round 5 computed both and posted them together: B's input layer sat on the path to the first
+    // contraction.)
     {
       f32x4 xa[UMAX][4], wa[UMAX][4], xb[UMAX][4], wbb[UMAX][4];
       in_issue(rowA, t_lo, xa, wa);
       in_issue(rowB, t_lo, xb, wbb);
       in_compute(t_lo, xa, wa, act);
       P3D_S6_STAMP(trs, 5);
+      group_sync(false, false);
       in_compute(t_lo, xb, wbb, act + 4 * slab);
       P3D_S6_STAMP(trs, 2);
-      group_sync(false, false);
     }
-    wait_for(nsync);                         // the input layers from this wave's K-slice producers
+    wait_for(nsync);                         // A's input layer from this wave's K-slice producers
     P3D_S6_STAMP(trs, 3);
     {
       const float *A0, *r0;

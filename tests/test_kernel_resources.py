@@ -67,8 +67,12 @@ def _find(res, name):
 def test_hot_kernel_uses_no_scratch(res, name):
     r = _find(res, name)
     assert r.get("private_segment_fixed_size", 0) == 0, (name, r)
-    # (SGPR spills go to VGPR lanes, v_writelane / v_readlane: no memory)
-    assert r.get("vgpr_spill_count", 0) == 0, (name, r)
+    # (SGPR spills go to VGPR lanes, v_writelane / v_readlane: no memory.)  VGPR spills: none, except
+    # into the accumulation registers -- the pair form's prologue spills 2 VGPRs while it holds unit
+    # B's input operands across unit A's post (round 6); with no scratch segment those can only be
+    # AGPR copies (v_accvgpr_write / read), never memory
+    spills = r.get("vgpr_spill_count", 0)
+    assert spills == 0 or (name.startswith("void k_serve6<4, 3, 2, 5, true>") and spills <= 2), (name, r)
     assert not r.get("uses_dynamic_stack", False), (name, r)
 
 
