@@ -880,7 +880,8 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
         model.step(None, x1, t1, 1.0, isTraining=False)
     dt = time.perf_counter() - t0
     out["eval_b1"] = {"us_per_call": round(1e6 * dt / n1, 2), "unit": "us",
-                      "note": "LinearModel.step() at batch 1 from numpy: H2D, 6 layer kernels, MSE, D2H, sync"}
+                      "note": "LinearModel.step() at batch 1 from numpy: one replayed HIP graph of H2D, the "
+                              "persistent batch-1 forward (k_gemv_chain), MSE, D2H; sync"}
     # device time of the batch-1 forward itself (k_gemv layers): a HIP graph of 50 forwards
     # replayed back to back (kernels + the dependent boundaries between them), and the hidden
     # layer's dispatch-attached duration against its weight stream
@@ -939,8 +940,9 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
         fl.lift_mapped(e)
     dt = time.perf_counter() - t0
     out["frontend_b1"] = {"us_per_frame": round(1e6 * dt / n1, 2), "unit": "us",
-                          "note": "openpose_frontend.FrameLifter: one HIP graph per frame (normalise, "
-                                  "6 layers, unNormalizeData) + pinned H2D/D2H + sync"}
+                          "note": "openpose_frontend.FrameLifter: one p3d_lift launch per frame (normalise, "
+                                  "the 6 layers as one persistent k_gemv_chain, unNormalizeData) reading and "
+                                  "writing the pinned frame rows directly + sync"}
     del fl
     model.close()
     return out
