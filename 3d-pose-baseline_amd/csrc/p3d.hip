@@ -115,7 +115,7 @@ struct p3d_model {
   int dgrad_out_wk = 4;       // waves of the output layer's dgrad launch (K = 48; env P3D_DGRAD_OUT_WK: 8, 4)
   int xchg_wk = 8;            // BN-train hidden exchange-form forward: 8 waves with an 8-deep ring (measured and
                               // pruned in round 4: 16 waves 8.6 vs 6.8 us; rings of 4 / 2 within 1 %)
-  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, 8, 4)
+  int dgrad_wk = 16;          // hidden data-gradient tiling (env P3D_DGRAD_WK: 16 waves, else 8)
   int train_xchg = 1;         // split BN-train layers as ONE launch when the grid fits (env P3D_TRAIN_XCHG, p3d_xchg.h)
   int num_cus = 0;            // compute units of the device (exchange-form residency bound)
   unsigned* xsync = nullptr;  // exchange form: per site (layer, direction) L/16 column-tile epoch words (one
@@ -171,9 +171,7 @@ struct p3d_model {
   int infer_wk = 82;        // inference tiling variant (launch_fwd_k), env P3D_INFER_WK
   int in_wk = 2, out_wk = 16; // input / output layer variants (env P3D_IN_WK, P3D_OUT_WK; 0 = infer_wk)
   int out_train_wk = 8;       // training output layer (fused MSE) variant (env P3D_OUT_TRAIN_WK)
-  int out_big = 0;            // output layer tiling at M >= big_m (env P3D_OUT_BIG; 0 = the B <= 64 one)
-  int train_wk = 8;         // waves per BN-train forward / dgrad workgroup (env P3D_TRAIN_WK)
-  int big_depth = 3;       // k_gemm_f32 LDS ring variant (see launch_big), env P3D_BIG_DEPTH
+  int train_wk = 8;         // waves per whole-batch BN-train workgroup (P3D_TRAIN_SPLIT=0 forms)
   int big_m = 256;          // inference hidden layers with M >= big_m use k_gemm_f32 (0: never)
   int gemv_maxb = 4;        // inference at B <= gemv_maxb runs the k_gemv layers (env P3D_GEMV_MAXB, 0..4)
   int gemv_fold = 1;        // ... with the input / output layers folded into the first / last hidden layer's
@@ -528,12 +526,10 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_IN_WK")) m->in_wk = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_WK")) m->out_wk = atoi(ev);
   if (const char* ev = getenv("P3D_OUT_TRAIN_WK")) m->out_train_wk = atoi(ev);
-  if (const char* ev = getenv("P3D_OUT_BIG")) m->out_big = atoi(ev);
   if (const char* ev = getenv("P3D_BIG_M")) m->big_m = atoi(ev);
   if (const char* ev = getenv("P3D_GEMV_MAXB")) m->gemv_maxb = std::max(0, std::min(4, atoi(ev)));
   if (const char* ev = getenv("P3D_GEMV_FOLD")) m->gemv_fold = atoi(ev);
   if (const char* ev = getenv("P3D_GEMV_CHAIN")) m->gemv_chain = atoi(ev);
-  if (const char* ev = getenv("P3D_TRAIN_WK")) m->train_wk = atoi(ev) == 16 ? 16 : 8;
   if (const char* ev = getenv("P3D_TRAIN_SPLIT")) m->train_split = atoi(ev);
   if (const char* ev = getenv("P3D_IN_TRAIN_WK")) m->in_train_wk = atoi(ev);
   if (const char* ev = getenv("P3D_DGRAD_OUT_WK")) m->dgrad_out_wk = atoi(ev);
@@ -590,7 +586,6 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
-  if (const char* ev = getenv("P3D_BIG_DEPTH")) m->big_depth = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6")) m->serve6 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_MAX_NB")) m->serve6_max_nb = atoi(ev);
@@ -769,24 +764,15 @@ template <bool APK, bool YPK, int KIND>
 static void launch_fwd_k(const ProfScope& ps, const FwdArgs& a, bool whole_batch, int wk, hipStream_t st) {
   const int gx = (a.N + 15) / 16;
   if (whole_batch) {
-    if (wk == 16) go(ps, k_fwd<4, 16, 4, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(1024), st, a);
-    else go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
+    go(ps, k_fwd<4, 8, 8, 2, APK, YPK, KIND>, dim3(gx, 1), dim3(512), st, a);
   } else {
-    // tiling variants (P3D_INFER_WK): 8 = 1 row tile x 8 waves (default), 16 = 16 waves,
-    // 84 = 8 waves with a 4-group register ring, 28 = 2 row tiles x 8 waves, 216 = 2 x 16
-    const int gy = (a.M + 15) / 16, gy2 = (a.M + 31) / 32;
+    // tiling variants (P3D_INFER_WK): 82 = 1 row tile x 8 waves, 2-group register ring (the
+    // inference default), 8 = the same with an 8-group ring (the training output layer), else 16
+    // waves with a 4-group ring (the inference output layer).  (Round 6 removed the ten other
+    // tilings the round-1 sweeps had measured slower.)
+    const int gy = (a.M + 15) / 16;
     if (wk == 8) go(ps, k_fwd<1, 8, 8, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 84) go(ps, k_fwd<1, 8, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 85) go(ps, k_fwd<1, 8, 3, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 86) go(ps, k_fwd<1, 8, 3, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
     else if (wk == 82) go(ps, k_fwd<1, 8, 2, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 80) go(ps, k_fwd<1, 8, 1, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 83) go(ps, k_fwd<1, 8, 2, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 81) go(ps, k_fwd<1, 8, 4, 1, APK, YPK, KIND>, dim3(gx, gy), dim3(512), st, a);
-    else if (wk == 44) go(ps, k_fwd<1, 4, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(256), st, a);
-    else if (wk == 162) go(ps, k_fwd<1, 16, 2, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(1024), st, a);
-    else if (wk == 28) go(ps, k_fwd<2, 8, 4, 2, APK, YPK, KIND>, dim3(gx, gy2), dim3(512), st, a);
-    else if (wk == 216) go(ps, k_fwd<2, 16, 2, 2, APK, YPK, KIND>, dim3(gx, gy2), dim3(1024), st, a);
     else go(ps, k_fwd<1, 16, 4, 2, APK, YPK, KIND>, dim3(gx, gy), dim3(1024), st, a);
   }
 }
@@ -814,11 +800,9 @@ static void launch_big(p3d_model* m, const FwdArgs& a, hipStream_t st) {
   const GemmF32Args g = big_args(a);
   const unsigned grid = (unsigned)(((a.M + 127) / 128) * (a.N / 128));
   ProfScope ps(m, "fwd_hidden_big");
-  // big_depth selects the LDS ring: 1 -> 1 k-group x 4 stages (64 KB, two workgroups per
-  // CU), 2 -> 2 k-groups x 3 stages (96 KB), 3 -> 2 k-groups x 2 stages (64 KB)
-  if (m->big_depth == 2) go(ps, k_gemm_f32<2, 3>, dim3(grid), dim3(256), st, g);
-  else if (m->big_depth == 3) go(ps, k_gemm_f32<2, 2>, dim3(grid), dim3(256), st, g);
-  else go(ps, k_gemm_f32<1, 4>, dim3(grid), dim3(256), st, g);
+  // the LDS ring: 2 k-groups x 2 stages (64 KB); (1 k-group x 4 stages and 2 x 3 stages measured
+  // slower in round 1 and were removed in round 6)
+  go(ps, k_gemm_f32<2, 2>, dim3(grid), dim3(256), st, g);
 }
 
 // BN-train layer, split form: 16x16 GEMM tiles (256 workgroups at L = 1024, B = 64) write z
@@ -899,18 +883,6 @@ static int launch_fwd(p3d_model* m, const FwdArgs& a, int kind, bool whole_batch
     // input layer (K = 32: two k-groups) at large M: 64 rows x 16 columns per wave
     ProfScope ps(m, "fwd_in_big");
     go(ps, k_fwd<4, 2, 2, 2, false, true, 0>, dim3((a.N + 15) / 16, (a.M + 63) / 64), dim3(128), st, a);
-    LAUNCH_CHECK("k_fwd");
-    return P3D_OK;
-  }
-  if (kind == 2 && !whole_batch && m->big_m > 0 && a.M >= m->big_m && m->out_big && !a.tgt && !a.z_save) {
-    // output layer (N = 48) at large M: several row tiles per wave so each weight fragment
-    // loaded serves 2-4 row tiles (P3D_OUT_BIG selects the tiling)
-    ProfScope ps(m, "fwd_out_big");
-    const int gx = (a.N + 15) / 16;
-    if (m->out_big == 1) go(ps, k_fwd<4, 8, 4, 2, true, false, 2>, dim3(gx, (a.M + 63) / 64), dim3(512), st, a);
-    else if (m->out_big == 2) go(ps, k_fwd<4, 16, 2, 2, true, false, 2>, dim3(gx, (a.M + 63) / 64), dim3(1024), st, a);
-    else if (m->out_big == 3) go(ps, k_fwd<2, 8, 4, 2, true, false, 2>, dim3(gx, (a.M + 31) / 32), dim3(512), st, a);
-    else go(ps, k_fwd<2, 16, 2, 2, true, false, 2>, dim3(gx, (a.M + 31) / 32), dim3(1024), st, a);
     LAUNCH_CHECK("k_fwd");
     return P3D_OK;
   }
@@ -1778,7 +1750,6 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
           // 16 waves (both BN forms, so they keep giving the same bits): 6.8 vs 7.0-7.1 us per
           // hidden dgrad (A/B, one box)
           if (m->dgrad_wk == 16) go(ps, k_dgrad<1, 16, 4, 2, true, 1>, g, dim3(1024), st, a);
-          else if (m->dgrad_wk == 4) go(ps, k_dgrad<1, 4, 4, 2, true, 1>, g, dim3(256), st, a);
           else go(ps, k_dgrad<1, 8, 8, 2, true, 1>, g, dim3(512), st, a);
         } else {
           dim3 g = grid;
@@ -1801,13 +1772,8 @@ extern "C" int p3d_backward(p3d_model* m, const float* dy, int64_t B, void* stre
       {
         ProfScope ps(m, is_out ? "dgrad_out" : "dgrad_hidden");
         const dim3 grid((a.K + 15) / 16, 1);
-        if (m->train_wk == 16) {
-          if (dz_pk) go(ps, k_dgrad<4, 16, 4, 2, true, 1>, grid, dim3(1024), st, a);
-          else go(ps, k_dgrad<4, 16, 4, 2, false, 2>, grid, dim3(1024), st, a);
-        } else {
-          if (dz_pk) go(ps, k_dgrad<4, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
-          else go(ps, k_dgrad<4, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
-        }
+        if (dz_pk) go(ps, k_dgrad<4, 8, 8, 2, true, 1>, grid, dim3(512), st, a);
+        else go(ps, k_dgrad<4, 8, 8, 2, false, 2>, grid, dim3(512), st, a);
       }
       LAUNCH_CHECK("k_dgrad");
     }
@@ -2139,21 +2105,11 @@ extern "C" int p3d_kernel_name(const p3d_model* m, int32_t what, char* out, int6
   if (what == 0) {
     switch (m->infer_wk) {
       case 8: n = "k_fwd<1, 8, 8, 2, true, true, 1>"; break;
-      case 84: n = "k_fwd<1, 8, 4, 2, true, true, 1>"; break;
-      case 85: n = "k_fwd<1, 8, 3, 2, true, true, 1>"; break;
-      case 86: n = "k_fwd<1, 8, 3, 1, true, true, 1>"; break;
       case 82: n = "k_fwd<1, 8, 2, 2, true, true, 1>"; break;
-      case 80: n = "k_fwd<1, 8, 1, 2, true, true, 1>"; break;
-      case 83: n = "k_fwd<1, 8, 2, 1, true, true, 1>"; break;
-      case 81: n = "k_fwd<1, 8, 4, 1, true, true, 1>"; break;
-      case 44: n = "k_fwd<1, 4, 4, 2, true, true, 1>"; break;
-      case 162: n = "k_fwd<1, 16, 2, 2, true, true, 1>"; break;
-      case 28: n = "k_fwd<2, 8, 4, 2, true, true, 1>"; break;
-      case 216: n = "k_fwd<2, 16, 2, 2, true, true, 1>"; break;
       default: n = "k_fwd<1, 16, 4, 2, true, true, 1>"; break;
     }
   } else if (what == 1) {
-    n = m->big_depth == 2 ? "k_gemm_f32<2, 3>" : m->big_depth == 3 ? "k_gemm_f32<2, 2>" : "k_gemm_f32<1, 4>";
+    n = "k_gemm_f32<2, 2>";
   } else if (what == 6) {
     // the optimizers' weight source (bench.py's byte count): "packed" = W read from its Wd copy, the
     // TF-layout master not written (28 B per weight element per fused step); "master" = 32 B
