@@ -389,12 +389,20 @@ def bench_serve(args, rank, world):
     # reported time is the MEDIAN repeat
     nrep = int(os.environ.get("P3D_BENCH_REPEATS", "9"))
     samples = []
+    # Each repeat: barrier + synchronize, t0, the K steps, this rank's synchronize, t1, then the
+    # closing barrier + synchronize; the repeat's time is the MAX over ranks of t1 - t0.  (At N > 1
+    # the closing barrier is an NCCL all-reduce whose own latency -- tens of us at 8 ranks, against
+    # a ~110 us region -- would otherwise sit inside every rank's interval; a slow rank still sets
+    # the repeat's time through the max.  At N = 1 both orders time the same interval.)
+    import torch
     for _ in range(max(1, nrep)):
         barrier_sync(world)
         t0 = time.perf_counter()
         run(R)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         barrier_sync(world)
-        samples.append(max_over_ranks(time.perf_counter() - t0, world))
+        samples.append(max_over_ranks(t1 - t0, world))
     dt = sorted(samples)[len(samples) // 2]
     model.serve_check()
     value = world * args.steps * BATCH / dt
