@@ -51,6 +51,7 @@ SIGNATURES = [
                                  c_uint64, c_int64, c_int64, c_void_p]),
     ("p3d_serve", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("p3d_serve_mse", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("p3d_serve_mse_sync", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("p3d_serve_check", c_int32, [c_void_p]),
     ("p3d_sync_check", c_int32, [c_void_p]),
     ("p3d_error_flags", c_int32, [c_void_p, POINTER(c_int32), c_int32]),
@@ -92,6 +93,8 @@ SIGNATURES = [
                                   c_void_p, c_void_p]),
     ("p3d_lift", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                            c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    ("p3d_lift_sync", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     ("p3d_moments_workspace", c_int64, [c_int64, c_int32]),
     ("p3d_moments", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     ("p3d_crc32c", c_uint32, [c_void_p, c_int64, c_uint32]),

@@ -129,6 +129,14 @@ struct p3d_model {
   int* errw = nullptr;        // host view
   int* xerr = nullptr;        // device view of errw[0]
   int* serve_err = nullptr;   // device view of errw[1]
+  // completion word of the *_sync calls (errw[8]; p3d_serve_mse_sync, p3d_lift_sync): the launch's
+  // last output writer stores the call's sequence number there once its host-memory outputs are
+  // system-visible, and the host spins on it instead of waiting for the runtime's completion signal
+  unsigned* hflag_dev = nullptr;   // device view of errw[8]
+  unsigned hseq = 0;               // last sequence number issued
+  unsigned hwait = 0;              // the sequence number the launch being built stores (0: none)
+  bool harmed = false;             // the launch just built carries it
+  unsigned* hcnt = nullptr;        // device arrival counter of those launches (zero between them)
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
   float* aff = nullptr;             // BN-eval affine per BN layer
@@ -301,6 +309,7 @@ void free_all(p3d_model* m) {
   if (m->gemv_epoch) (void)hipFree(m->gemv_epoch);
   if (m->errw) (void)hipHostFree(m->errw);
   if (m->alpha_dev) (void)hipFree(m->alpha_dev);
+  if (m->hcnt) (void)hipFree(m->hcnt);
   for (hipEvent_t e : m->rev) (void)hipEventDestroy(e);
   m->rev.clear();
   if (m->cjoin) (void)hipEventDestroy(m->cjoin);
@@ -571,6 +580,7 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
     if ((e = hipHostGetDevicePointer((void**)&dv, m->errw, 0)) != hipSuccess) return cleanup(e);
     m->xerr = dv;
     m->serve_err = dv + 1;
+    m->hflag_dev = (unsigned*)(dv + 8);
   }
   if (const char* ev = getenv("P3D_XCHG_TEST_DELAY")) m->xchg_delay = atoi(ev);
   if (const char* ev = getenv("P3D_DP_ADAM")) m->dp_adam = atoi(ev);
@@ -586,6 +596,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
+  if ((e = hipMalloc(&m->hcnt, 64 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->hcnt, 0, 64 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6")) m->serve6 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_MAX_NB")) m->serve6_max_nb = atoi(ev);
@@ -1027,7 +1039,11 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
     ch.hand = m->gemv_hand + slot * m->gemv_slot_floats;
     ch.epoch = m->gemv_epoch + slot * P3D_XCHG_EPOCH_STRIDE;
     ch.err = m->xerr;
-    if (fr) { ch.fr = *fr; ch.out.Y = nullptr; }
+    if (fr) {
+      ch.fr = *fr;
+      ch.out.Y = nullptr;
+      if (ch.fr.hflag) ch.fr.hcount = (ch.out.N + 15) >> 4;   // the output-tile workgroups (p3d_gemv.h)
+    }
     {
       ProfScope ps(m, "gemv_chain");
       go(ps, k_gemv_chain<4, 4>, dim3((unsigned)(H * T)), dim3(1024), st, ch);
@@ -1436,6 +1452,7 @@ static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const f
   if (t) {
     a.tgt = t; a.loss = loss;
     a.lpart = m->serve_loss; a.lcnt = (unsigned*)(m->serve_loss + P3D_SERVE6_ROWS / 16 * 4);
+    if (m->hwait && use6 && !plan.pair) { a.hflag = m->hflag_dev; a.hseq = m->hwait; m->harmed = true; }
   }
   if (use6) {
     a.act = m->serve6_act;                   // [group][4 slabs][16 RT rows][L]; no output partials
@@ -2325,7 +2342,9 @@ extern "C" int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, 
     GemvFrames fr{};
     fr.raw = raw; fr.ldraw = D2; fr.mean2 = mean2; fr.std2 = std2; fr.use2 = use2;
     fr.out = out; fr.D3 = D3; fr.mean3 = mean3; fr.std3 = std3; fr.use3 = use3;
+    if (m->hwait) { fr.hflag = m->hflag_dev; fr.hcnt = m->hcnt; fr.hseq = m->hwait; }
     const int r = forward_gemv(m, nullptr, B, nullptr, 1.0f, 0, 0, 0, 0, st, &fr);   // (keep 1: no dropout, seed unused)
+    if (r == P3D_OK && m->hwait) m->harmed = true;
     if (r != 1) return r;
   }
   int r = p3d_normalize(raw, B, D2, mean2, std2, use2, U2, m->lift_x, P3D_DTYPE_F32, stream);
@@ -2333,6 +2352,81 @@ extern "C" int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, 
   r = forward_impl(m, m->lift_x, B, m->lift_y, 0, 1.0f, 0, 0, 0, 0, stream, nullptr);
   if (r) return r;
   return p3d_unnormalize(m->lift_y, P3D_DTYPE_F32, B, U3, mean3, std3, use3, D3, out, stream);
+}
+
+// ---- the *_sync calls: launch, then wait for the results in host memory --------------------------
+// The launch's last output writer stores the call's sequence number into the completion word (errw[8],
+// pinned and coherent) once its host-memory outputs are system-visible; the host spins on that word
+// instead of the runtime's completion signal (tools/flag_probe.hip on MI355X: 8.5 vs 13.6 us for a
+// one-workgroup kernel, 32.1 vs 37.8 us for 256 workgroups writing 256 KB of rows).  Every 4096 polls
+// the stream is queried, so a launch that ends without storing the word (a fault, a launch whose
+// workgroups could not synchronise) is reported instead of waited for.  The stream's own completion
+// is not waited for: later work on it is ordered behind the launch as usual.
+static int host_wait(p3d_model* m, unsigned seq, hipStream_t st, const char* what) {
+  unsigned* word = reinterpret_cast<unsigned*>(m->errw) + 8;
+  for (uint64_t n = 1;; ++n) {
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return P3D_OK;
+    if ((n & 4095) == 0) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return P3D_OK;
+        return fail(P3D_ERR_HIP, std::string(what) + ": the launch completed without storing its completion word");
+      }
+      if (e != hipErrorNotReady) return fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    }
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
+// arm the next launch with a fresh sequence number; refuses a capturing stream (a replayed graph
+// would store a stale number)
+static int host_arm(p3d_model* m, hipStream_t st, const char* what, unsigned& seq) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const hipError_t e = hipStreamIsCapturing(st, &cap);
+  if (e != hipSuccess) return fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  if (cap != hipStreamCaptureStatusNone) return fail(P3D_ERR_STATE, std::string(what) + ": not capturable (waits on the host)");
+  if (++m->hseq == 0) ++m->hseq;
+  seq = m->hseq;
+  m->hwait = seq;
+  m->harmed = false;
+  return P3D_OK;
+}
+
+static int host_finish(p3d_model* m, int rc, unsigned seq, hipStream_t st, const char* what) {
+  const bool armed = m->harmed;
+  m->hwait = 0;
+  m->harmed = false;
+  if (rc) return rc;
+  if (!armed) {   // a form without the completion word: the runtime's completion
+    const hipError_t e = hipStreamSynchronize(st);
+    return e == hipSuccess ? P3D_OK : fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
+  return host_wait(m, seq, st, what);
+}
+
+// (include/p3d.h) p3d_serve_mse, returning once y and *loss hold the results
+extern "C" int p3d_serve_mse_sync(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss,
+                                  void* stream) {
+  if (!m || !t || !loss) return fail(P3D_ERR_ARG, "p3d_serve_mse_sync: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  unsigned seq = 0;
+  if (int rc = host_arm(m, st, "p3d_serve_mse_sync", seq)) return rc;
+  return host_finish(m, serve_impl(m, x, B, y, t, loss, stream), seq, st, "p3d_serve_mse_sync");
+}
+
+// (include/p3d.h) p3d_lift, returning once out holds the results
+extern "C" int p3d_lift_sync(p3d_model* m, const double* raw, int64_t B, int32_t D2, const double* mean2,
+                             const double* std2, const int32_t* use2, int32_t U2, const double* mean3,
+                             const double* std3, const int32_t* use3, int32_t U3, int32_t D3, double* out,
+                             void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_lift_sync: null model");
+  hipStream_t st = (hipStream_t)stream;
+  unsigned seq = 0;
+  if (int rc = host_arm(m, st, "p3d_lift_sync", seq)) return rc;
+  return host_finish(m, p3d_lift(m, raw, B, D2, mean2, std2, use2, U2, mean3, std3, use3, U3, D3, out, stream), seq, st,
+                     "p3d_lift_sync");
 }
 
 extern "C" int64_t p3d_moments_workspace(int64_t F, int32_t D) {

@@ -58,7 +58,25 @@ struct GemvFrames {
   const double* mean2; const double* std2; const int32_t* use2;      // use2: in.K columns of raw
   double* out; int D3;                                               // [M][D3] float64 (null: off)
   const double* mean3; const double* std3; const int32_t* use3;      // use3: out.N columns of out
+  // p3d_lift_sync: host-visible completion word (pinned, coherent; null: off), the call's sequence
+  // number, a device arrival counter (zero between launches) and the launch's output workgroups
+  unsigned* hflag; unsigned* hcnt; unsigned hseq; int hcount;
 };
+
+// The host-completion arrival of one output workgroup (whole workgroup, uniform call): each
+// thread's host-memory stores made system-visible, then one arrival; the last arriver resets the
+// counter and stores the call's sequence number into the host word (system-scope release).
+__device__ __forceinline__ void p3d_host_arrive(const GemvFrames& fr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (system scope: no acquire half, no cache invalidate)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(fr.hcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)prev + 1 == fr.hcount) {
+      __hip_atomic_store(fr.hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fr.hflag, fr.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
 
 // ---- the layer epilogue of k_fwd for one (row, column) ---------------------------------------
 struct GemvEpi {
@@ -474,21 +492,23 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
   // every wave has seen its producers' granules, so every workgroup of the launch has read the
   // epoch (each producer tagged with it): the slot's next launch gets a new tag
   if (threadIdx.x == 0 && t0 == 0) __hip_atomic_fetch_add(f.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (w != 0 || q >= M || q >= MR) return;
+  if (w == 0 && q < M && q < MR) {
 #pragma unroll
-  for (int u = 0; u < NTO; ++u) {
-    const int t = t0 + u;
-    if (t >= t1) break;
-    const int col = 16 * t + i;
-    float zs = 0.f;
+    for (int u = 0; u < NTO; ++u) {
+      const int t = t0 + u;
+      if (t >= t1) break;
+      const int col = 16 * t + i;
+      float zs = 0.f;
 #pragma unroll
-    for (int v = 0; v < WV; ++v) zs += red[u][v][q][i];
-    const float y = p3d_gemv_epi(o, e[u], zs, q, col < o.N ? col : o.N - 1);
-    if (col < o.N) {
-      if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
-      if (f.fr.out) f.fr.out[(int64_t)q * f.fr.D3 + od[col]] = p3d_unnorm_out(y, osd[col], omu[col]);
+      for (int v = 0; v < WV; ++v) zs += red[u][v][q][i];
+      const float y = p3d_gemv_epi(o, e[u], zs, q, col < o.N ? col : o.N - 1);
+      if (col < o.N) {
+        if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
+        if (f.fr.out) f.fr.out[(int64_t)q * f.fr.D3 + od[col]] = p3d_unnorm_out(y, osd[col], omu[col]);
+      }
     }
   }
+  if (f.fr.hflag) p3d_host_arrive(f.fr);
 }
 
 // A hidden layer as k_gemv<MR, WV, GC> (the same bits), with the input layer folded in ahead of it

@@ -127,6 +127,11 @@ struct ServeArgs {
   float* lpart;
   unsigned* lcnt;
   float* loss;
+  // p3d_serve_mse_sync: host-visible completion word (pinned, coherent; null: off) and the call's
+  // sequence number, stored by the last arriving tile once every output row and the loss are
+  // system-visible (each tile's wave fences its own rows at system scope before it arrives)
+  unsigned* hflag;
+  unsigned hseq;
   ServeLayer ly[P3D_SERVE_MAXL];
 };
 
@@ -424,11 +429,15 @@ __device__ __forceinline__ f32x4 p3d_serve_load_tgt(const ServeArgs& p, int e4, 
 // order (lane l: tiles l, l + 64, ...; then the same butterfly) and writes mean = sum / (M ND); it
 // resets the counter for the next launch (stream-ordered behind this one).  Same bits for the same
 // launch shape; tiles past the last row (a pair unit past the end) do not arrive.
+// HF: the form may carry the host completion word (p3d_serve_mse_sync; not the pair form, whose
+// register budget has no room for the fence path -- that form's sync call waits on the stream).
+template <bool HF>
 __device__ __forceinline__ void p3d_serve_loss_tile(const ServeArgs& p, float se, int64_t gtile, int64_t ntiles) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) se += __shfl_xor(se, o, 64);
   if (gtile >= ntiles) return;
+  if (HF && p.hflag) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's rows (host memory): system-visible
   unsigned v = 0;
   if (lane == 0) {
     __hip_atomic_store(p.lpart + gtile, se, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -444,6 +453,8 @@ __device__ __forceinline__ void p3d_serve_loss_tile(const ServeArgs& p, float se
   if (lane == 0) {
     *p.loss = t / (float)(p.M * p.ND);
     __hip_atomic_store(p.lcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (HF && p.hflag)   // every tile arrived after its fence: rows + loss are the host's once it reads hseq
+      __hip_atomic_store(p.hflag, p.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int64_t orow = tb ? orow1 : orow0;
         const float se = p3d_serve_store_out<NDT>(p, lo, tot, tile * 64 + lane, orow, tv);
         if (p.tgt)                             // fused MSE (p3d_serve_mse): this tile's share
-          p3d_serve_loss_tile(p, se, (orow >> 4) * NDT + tile, ((p.M + 15) >> 4) * NDT);
+          p3d_serve_loss_tile<!PAIR>(p, se, (orow >> 4) * NDT + tile, ((p.M + 15) >> 4) * NDT);
       }
       if (c0 == o_lo) P3D_S6_OSTAMP(2);
       __syncthreads();                         // red is rewritten next (next round / phase)

@@ -859,8 +859,13 @@ class LinearModel(object):
                   "hy_np": hout[:nt].view(B, self.output_size).numpy(), "hl_np": hout[nt:nt + 1].numpy()}
             args = (self._h, ctypes.c_void_p(hin.data_ptr()), B, ctypes.c_void_p(hout.data_ptr()),
                     ctypes.c_void_p(hin.data_ptr() + 4 * nx), ctypes.c_void_p(hout.data_ptr() + 4 * nt))
-            fn, sh = lib().p3d_serve_mse, _p3d.stream_handle
+            # p3d_serve_mse_sync returns once y and the loss are in the pinned buffers (it waits on
+            # the launch's completion word, not on the runtime's completion signal); env
+            # P3D_HOST_WAIT=0: p3d_serve_mse + a stream synchronize
+            host_wait = os.environ.get("P3D_HOST_WAIT", "1") != "0"
+            fn, sh = (lib().p3d_serve_mse_sync if host_wait else lib().p3d_serve_mse), _p3d.stream_handle
             st["launch"] = lambda: fn(*args, ctypes.c_void_p(sh()))   # noqa: E731
+            st["sync"] = not host_wait
             np.copyto(st["hx_np"], 0.0)
             np.copyto(st["ht_np"], 0.0)
             rc = st["launch"]()
@@ -895,7 +900,8 @@ class LinearModel(object):
                 rc = ss["launch"]()
                 if rc:
                     check(rc, "p3d_serve_mse")
-                self.torch.cuda.current_stream(self.device).synchronize()
+                if ss["sync"]:
+                    self.torch.cuda.current_stream(self.device).synchronize()
                 self.check_errors()
                 lv = float(ss["hl_np"][0])
                 return lv, Summary("loss/loss", lv), ss["hy_np"].copy()

@@ -80,7 +80,7 @@ class FrameLifter:
             self.y = torch.empty((self.B, model.output_size), dtype=f32, device=dev)
             self.p3 = torch.empty((self.B, D3), dtype=f64, device=dev)
             self.hin.zero_()
-            self.graph, self._launch = None, None
+            self.graph, self._launch, self._host_wait = None, None, False
             if not model.bf16 and os.environ.get("P3D_LIFT_EAGER", "1") != "0":
                 # fp32 (round 6): ONE p3d_lift launch per call that reads the pinned frame rows and
                 # writes the pinned millimetre rows itself (mapped host memory), its ctypes
@@ -91,7 +91,11 @@ class FrameLifter:
                 args = (model._h, c(self.hin.data_ptr()), self.B, 64, c(self.m2.data_ptr()), c(self.s2.data_ptr()),
                         c(self.u2.data_ptr()), self.u2.numel(), c(self.m3.data_ptr()), c(self.s3.data_ptr()),
                         c(self.u3.data_ptr()), self.u3.numel(), D3, c(self.hout.data_ptr()))
-                fn, sh = _p3d.lib().p3d_lift, _p3d.stream_handle
+                # p3d_lift_sync returns once the rows are in hout (the launch's output workgroups
+                # store a completion word the host waits on); env P3D_HOST_WAIT=0: p3d_lift + a
+                # stream synchronize
+                self._host_wait = os.environ.get("P3D_HOST_WAIT", "1") != "0"
+                fn, sh = (_p3d.lib().p3d_lift_sync if self._host_wait else _p3d.lib().p3d_lift), _p3d.stream_handle
                 self._launch = lambda: fn(*args, c(sh()))   # noqa: E731
                 _p3d.check(self._launch(), "p3d_lift")
                 torch.cuda.current_stream(dev).synchronize()
@@ -131,9 +135,11 @@ class FrameLifter:
             if rc:
                 import _p3d
                 _p3d.check(rc, "p3d_lift")
+            if not self._host_wait:
+                self.torch.cuda.current_stream(self.model.device).synchronize()
         else:
             self.graph.replay()
-        self.torch.cuda.current_stream(self.model.device).synchronize()
+            self.torch.cuda.current_stream(self.model.device).synchronize()
         return self.hout_np[:n].copy()
 
     def lift(self, frames_xy):

@@ -492,11 +492,30 @@ def serve_region_accounting(model, run, R, nrep, world):
     run(3)
     torch.cuda.synchronize()
     k = paired(lambda: run(R), "serve")
+
+    def plain(fn):   # the same region without the event pair (the headline's own form)
+        regions = []
+        for _ in range(max(3, nrep)):
+            barrier_sync(world)
+            t0 = time.perf_counter()
+            fn()
+            barrier_sync(world)
+            regions.append(1e6 * (time.perf_counter() - t0))
+        return round(sorted(regions)[len(regions) // 2], 2), [round(v, 1) for v in regions]
+    eu, eus = plain(empty)
+    su, sus = plain(lambda: run(R))
+    # without events: timed region = kernel + (empty region - empty kernel) + residual, with both
+    # kernels' device times from the paired repeats
     return {"serve_paired": k, "empty_kernel": e,
             "launch_completion_overhead_us": round(e["gap_us"], 2),
             "residual_us": round(k["gap_us"] - e["gap_us"], 2),
+            "unpaired": {"serve_region_us": su, "serve_regions_us": sus, "empty_region_us": eu, "empty_regions_us": eus,
+                         "launch_completion_overhead_us": round(eu - e["device_us"], 2),
+                         "residual_us": round((su - k["device_us"]) - (eu - e["device_us"]), 2)},
             "note": "gap = timed region - the kernel's event-timed device time, per repeat (median); the empty "
-                    "kernel's gap is the launch + completion round trip with no work; residual = serve gap - empty gap"}
+                    "kernel's gap is the launch + completion round trip with no work; residual = serve gap - empty gap; "
+                    "'unpaired' repeats both regions without the event pair (the headline's form) and subtracts the "
+                    "paired repeats' device times"}
 
 
 def bench_latency_b64(reps=300):

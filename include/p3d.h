@@ -141,6 +141,14 @@ int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
  * P3D_ERR_ARG where no k_serve6 form covers the launch (> 32 batch-64 steps, or a model shape
  * it is not built for): the caller uses p3d_serve + p3d_mse there. */
 int p3d_serve_mse(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss, void* stream);
+/* p3d_serve_mse that returns once y and *loss hold the results, for outputs in pinned host memory
+ * (the reference's session.run returns its fetches: src/linear_model.py:239-245).  The launch's last
+ * output tile stores the call's sequence number into a pinned completion word after every row and
+ * the loss are system-visible, and the host waits on that word rather than on the runtime's
+ * completion signal; the stream itself is not synchronised (later work on it is ordered behind the
+ * launch).  Not capturable (P3D_ERR_STATE on a capturing stream).  Errors as p3d_serve_mse, plus
+ * P3D_ERR_HIP when the launch ends without storing the word. */
+int p3d_serve_mse_sync(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss, void* stream);
 /* 0 if every p3d_serve launch so far completed its synchronisation (synchronises the device,
  * then reads the kernels' pinned error word).  After a failure p3d_serve refuses new launches
  * (P3D_ERR_HIP) until this call reports it once; the failed launch's rows hold NaN, never
@@ -378,6 +386,13 @@ int p3d_unnormalize(const void* xn, int32_t in_dtype, int64_t F, int32_t U, cons
 int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, const double* mean2, const double* std2,
              const int32_t* use2, int32_t U2, const double* mean3, const double* std3, const int32_t* use3,
              int32_t U3, int32_t D3, double* out, void* stream);
+/* p3d_lift that returns once out holds the results (pinned host rows; the per-frame call of
+ * src/openpose_3dpose_sandbox.py:353-356): on the one-launch chain form the launch's output
+ * workgroups store a completion word the host waits on, as p3d_serve_mse_sync; on the three-step
+ * form the stream is synchronised.  Not capturable. */
+int p3d_lift_sync(p3d_model* m, const double* raw, int64_t B, int32_t D2, const double* mean2, const double* std2,
+                  const int32_t* use2, int32_t U2, const double* mean3, const double* std3, const int32_t* use3,
+                  int32_t U3, int32_t D3, double* out, void* stream);
 
 /* np.mean / np.std (population) over axis 0 of x [F, D], D <= 256 -- the statistics of
  * src/data_utils.py:210-211 (normalization_stats).  Deterministic two-level column sums;

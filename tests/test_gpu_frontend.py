@@ -116,27 +116,34 @@ def test_frame_lifter_without_batch4_forms(env, monkeypatch):
 
 
 def test_frame_lifter_eager_equals_graph(monkeypatch):
-    """FrameLifter's one-launch path (round 6: p3d_lift on the pinned frame and output rows,
-    arguments bound once) == its HIP-graph path (P3D_LIFT_EAGER=0: H2D, p3d_lift, D2H), bit for
-    bit, at batch 1 and 4 (the chain) and 8 (the three calls)."""
+    """FrameLifter's one-launch path (round 6: p3d_lift_sync on the pinned frame and output rows,
+    arguments bound once, returning once the launch's completion word says the rows are in host
+    memory) == the same launch + a stream synchronize (P3D_HOST_WAIT=0) == its HIP-graph path
+    (P3D_LIFT_EAGER=0: H2D, p3d_lift, D2H), bit for bit, at batch 1 and 4 (the chain) and 8 (the
+    three calls, where the sync call waits on the stream) -- 6 calls on different frames each, so a
+    call returning the previous call's rows would show."""
     for B in (1, 4, 8):
         rng = np.random.default_rng(700 + B)
         use2, _ = data_utils.dimension_sets(2)
         _, ign3 = data_utils.dimension_sets(3)
         stats = (rng.uniform(200, 600, 64), rng.uniform(50, 150, 64), use2, rng.uniform(-400, 400, 96),
                  rng.uniform(30, 300, 96), ign3)
-        e = of.map_frames(rng.uniform(100, 900, (B, 36)))
+        frames = [of.map_frames(rng.uniform(100, 900, (B, 36))) for _ in range(6)]
         res = {}
-        for flag in ("1", "0"):
-            monkeypatch.setenv("P3D_LIFT_EAGER", flag)
+        for eager, hw in (("1", "1"), ("1", "0"), ("0", "1")):
+            monkeypatch.setenv("P3D_LIFT_EAGER", eager)
+            monkeypatch.setenv("P3D_HOST_WAIT", hw)
             cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
             st = ref_mlp.init_state(cfg, seed=1, bn_seed=2)
             m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_fl", seed=3, max_batch=64)
             m.set_weights({**st.params, **st.moving})
             fl = of.FrameLifter(m, *stats, batch=B)
-            assert (fl._launch is not None) == (flag == "1")
-            res[flag] = [fl.lift_mapped(e) for _ in range(2)]
+            assert (fl._launch is not None) == (eager == "1")
+            assert fl._host_wait == (eager == "1" and hw == "1")
+            res[eager + hw] = [fl.lift_mapped(e) for e in frames]
             del fl
             m.close()
-        np.testing.assert_array_equal(res["1"][0], res["0"][0])
-        np.testing.assert_array_equal(res["1"][1], res["1"][0])
+        for k in ("10", "01"):
+            for a, b in zip(res["11"], res[k]):
+                np.testing.assert_array_equal(a, b)
+        assert not np.array_equal(res["11"][0], res["11"][1])

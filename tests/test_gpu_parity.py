@@ -8,7 +8,9 @@ Tolerances (fp32 path vs fp64 oracle):
   pre-BN biases are not compared element-wise after Adam: their gradient is
   analytically zero under batch-norm and Adam normalises its rounding noise
   ("pre-BN bias"); test_train_steps_track_oracle bounds them on both
-  sides by Adam's step bound instead.
+  sides by Adam's step bound, and test_optimizer_elementwise_on_device_gradients
+  checks their gradient is rounding-sized and their update element by element
+  (TF1 Adam applied to the device's own gradient).
 """
 import os
 
@@ -244,6 +246,81 @@ def test_train_steps_track_oracle(split, xchg, monkeypatch):
             continue
         err = np.abs(w[name] - st.params[name]).max()
         assert err < 5e-5, (name, err)
+    m.close()
+
+
+def test_optimizer_elementwise_on_device_gradients():
+    """Element-wise check of every variable's update, the pre-BN biases included (they
+    were only bounded).  A pre-BN bias's gradient is the batch sum of BN's input gradient -- zero up
+    to rounding -- so neither side's value is reproducible by the other; what IS defined:
+      * that gradient is rounding-sized: <= 1e-4 x the gradient of the same layer's BN beta;
+      * TF1 ApplyAdam (oracle adam_apply's formula, float64) applied to the device's OWN gradient
+        reproduces the device's Adam m and v element by element within their float32 rounding,
+        and the device's new weight from those slots within 1 ulp + 1e-6 of the update, for every
+        trainable, over 5 steps of the data-parallel form's separate optimizer
+        (p3d_train_fwd_bwd_lr + p3d_adam_apply; the fused step shares p3d_adam1 and is checked
+        bit-identical to it by test_optimizer_from_packed_weights_bit_identical)."""
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st = ref_mlp.init_state(cfg, seed=6, bn_seed=7)
+    m = linear_model.LinearModel(1024, 2, True, True, False, 64, 1e-3, "/tmp/p3d_prebn", seed=9, max_batch=64)
+    m.set_weights({**st.params, **st.moving})
+    names = m.trainable_names()
+    pre = [n for n in names if "/b1" in n or "/b2_" in n or "/b3_" in n]
+    assert len(pre) == 5
+    rng = np.random.default_rng(31)
+    y = torch.empty((64, 48), device="cuda")
+    loss = torch.empty(1, device="cuda")
+    f64 = np.float64
+    # TF1's ApplyAdam forms 1 - beta in the variable's dtype from float32 constants: 1 - 0.999f is
+    # 9.99987e-4, 1.3e-5 away from 1e-3 -- the device does the same, so the float64 reference below
+    # takes the float32 constants too
+    f32 = np.float32
+    omb1, omb2 = f64(f32(1.0) - f32(ref_mlp.ADAM_B1)), f64(f32(1.0) - f32(ref_mlp.ADAM_B2))
+    eps = f64(f32(ref_mlp.ADAM_EPS))
+    for step in range(5):
+        s0 = m.get_state()
+        x = torch.from_numpy(rng.standard_normal((64, 32)).astype(np.float32)).cuda()
+        t = torch.from_numpy(rng.standard_normal((64, 48)).astype(np.float32)).cuda()
+        _p3d.check(_p3d.lib().p3d_train_fwd_bwd_lr(m._h, _p3d.ptr(x), _p3d.ptr(t), 64, _p3d.ptr(y), 0.5, m.seed, 0,
+                                                   1e-3, 100000.0, 0.96, _p3d.ptr(loss), m.stream()))
+        torch.cuda.synchronize()
+        g = {n: m.grad(n).cpu().numpy().astype(f64) for n in names}
+        _p3d.check(_p3d.lib().p3d_adam_apply(m._h, m.stream()))
+        torch.cuda.synchronize()
+        s1 = m.get_state()
+        assert int(s1["global_step"]) == int(s0["global_step"]) + 1
+        lr = f64(ref_mlp.decayed_lr(1e-3, int(s0["global_step"])))
+        alpha = lr * np.sqrt(1.0 - f64(s0["beta2_power"])) / (1.0 - f64(s0["beta1_power"]))
+        for n in pre:
+            beta = names[names.index(n) + 2]
+            assert beta.endswith("/beta"), beta
+            assert np.abs(g[n]).max() <= 1e-4 * np.abs(g[beta]).max(), (step, n, np.abs(g[n]).max())
+        u = 2.0 ** -24   # float32 unit roundoff
+        for n in names:
+            m0, v0 = s0[n + "/Adam"].astype(f64), s0[n + "/Adam_1"].astype(f64)
+            m1, v1 = s1[n + "/Adam"].astype(f64), s1[n + "/Adam_1"].astype(f64)
+            mr = m0 + (g[n] - m0) * omb1
+            vr = v0 + (g[n] * g[n] - v0) * omb2
+            # the slots: within the float32 rounding of their three / four operations, per element
+            # (m = m + (g - m)(1 - b1) cancels where g ~ -9 m: the bound scales with the operands)
+            em = 4 * u * (np.abs(m0) + np.abs(g[n] - m0) * omb1 + np.abs(mr))
+            ev = 4 * u * (np.abs(v0) + (g[n] * g[n] + np.abs(v0)) * omb2 + np.abs(vr))
+            assert np.all(np.abs(m1 - mr) <= em), (step, n, "m", np.abs(m1 - mr).max())
+            assert np.all(np.abs(v1 - vr) <= ev), (step, n, "v", np.abs(v1 - vr).max())
+            # the weight from the device's own slots: w -= (m alpha) / (sqrt(v) + eps), float32 rounding
+            # of its last subtraction (1 ulp of w) plus 1e-6 of the update (alpha's float32 formation,
+            # the sqrt, the division)
+            upd = (m1 * alpha) / (np.sqrt(v1) + eps)
+            wr = s0[n].astype(f64) - upd
+            tol = np.spacing(np.abs(wr).astype(np.float32)).astype(f64) + 1e-6 * np.abs(upd)
+            bad = np.abs(s1[n].astype(f64) - wr) > tol
+            if bad.any():
+                i = np.unravel_index(np.argmax(np.abs(s1[n].astype(f64) - wr) - tol), wr.shape)
+                print("DIAG", step, n, i, "w0", float(s0[n][i]), "g", g[n][i], "m1", m1[i], "v1", v1[i],
+                      "w1", float(s1[n][i]), wr[i], "upd", upd[i], "alpha", alpha, "nbad", int(bad.sum()))
+            assert not bad.any(), (step, n, np.abs(s1[n].astype(f64) - wr).max())
+    m.check_errors()
     m.close()
 
 

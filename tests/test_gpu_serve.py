@@ -460,3 +460,60 @@ def test_step_eval_one_launch_path_and_fallback():
         close(out, ro)
         assert abs(loss - rl) <= 1e-5 * max(1.0, abs(rl)), (B, loss, rl)
     m.close()
+
+
+@pytest.mark.parametrize("B", [64, 37, 300, 1280])
+def test_serve_mse_sync_returns_with_results_in_host_memory(B):
+    """p3d_serve_mse_sync (round 6): returns once y and the loss are in the pinned buffers -- the
+    launch's last output tile stores a completion word the host waits on (B = 1280: the pair form,
+    which carries no word, waits on the stream instead).  Read straight after the call, with no
+    synchronize, 12 calls on fresh inputs each equal p3d_serve_mse's results on the same inputs
+    (stream-synchronised) bit for bit -- a result of the previous call would show as a mismatch."""
+    import ctypes
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg, max_batch=max(B, 64))
+    c = ctypes.c_void_p
+    hx = torch.empty((B, 32), dtype=torch.float32).pin_memory()
+    ht = torch.empty((B, 48), dtype=torch.float32).pin_memory()
+    hy = torch.empty((B, 48), dtype=torch.float32).pin_memory()
+    hl = torch.zeros(4, dtype=torch.float32).pin_memory()
+    ry = torch.empty((B, 48), dtype=torch.float32).pin_memory()
+    rl = torch.zeros(4, dtype=torch.float32).pin_memory()
+    rng = np.random.default_rng(B + 17)
+    lib = _p3d.lib()
+    for it in range(12):
+        hx.copy_(torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)))
+        ht.copy_(torch.from_numpy(rng.standard_normal((B, 48)).astype(np.float32)))
+        _p3d.check(lib.p3d_serve_mse_sync(m._h, c(hx.data_ptr()), B, c(hy.data_ptr()), c(ht.data_ptr()),
+                                          c(hl.data_ptr()), c(_p3d.stream_handle())), "p3d_serve_mse_sync")
+        got_y, got_l = hy.numpy().copy(), float(hl[0])
+        _p3d.check(lib.p3d_serve_mse(m._h, c(hx.data_ptr()), B, c(ry.data_ptr()), c(ht.data_ptr()),
+                                     c(rl.data_ptr()), c(_p3d.stream_handle())), "p3d_serve_mse")
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(got_y, ry.numpy(), err_msg="call %d" % it)
+        assert got_l == float(rl[0]), (it, got_l, float(rl[0]))
+    m.serve_check()
+    m.check_errors()
+    ro, _ = ref_mlp.forward(st, hx.numpy().astype(np.float64), False, 1.0, 0, 0, 0)
+    close(hy.numpy(), ro)
+    m.close()
+
+
+def test_step_eval_host_wait_equals_stream_sync(monkeypatch):
+    """LinearModel.step(isTraining=False) at B = 64 through p3d_serve_mse_sync (default) and through
+    p3d_serve_mse + a stream synchronize (P3D_HOST_WAIT=0): 10 steps on fresh inputs, the same
+    outputs and loss bit for bit, step by step."""
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    res = {}
+    for hw in ("1", "0"):
+        monkeypatch.setenv("P3D_HOST_WAIT", hw)
+        st, m = make(cfg)
+        rng = np.random.default_rng(77)
+        res[hw] = [m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 1.0, isTraining=False)
+                   for _ in range(10)]
+        assert m._serve_steps[64]["sync"] == (hw == "0")
+        m.close()
+    for (la, _, ya), (lb, _, yb) in zip(res["1"], res["0"]):
+        assert la == lb
+        np.testing.assert_array_equal(ya, yb)

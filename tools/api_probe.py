@@ -5,7 +5,8 @@
 (1) LinearModel.step(isTraining=False) at B = 64 from numpy, as shipped; (2) its pieces; (3) eager
 alternatives: p3d_serve reading x straight from pinned host memory and writing y there (zero-copy),
 p3d_mse on the pinned buffers, one synchronize; the same with device buffers and explicit copies;
-(4) FrameLifter (graph per frame) vs an eager p3d_lift on the pinned buffers.  Prints JSON."""
+(4) FrameLifter as shipped (p3d_lift_sync), from mapped rows and from an OpenPose frame, vs p3d_lift
+on the pinned buffers + a stream synchronize.  Prints JSON."""
 import json
 import os
 import sys
@@ -96,7 +97,11 @@ def main():
     if ss is not None:
         np.copyto(ss["hx_np"], x, casting="unsafe")
         np.copyto(ss["ht_np"], t, casting="unsafe")
-        out["serve_mse_launch_sync"] = med(lambda: (ss["launch"](), torch.cuda.current_stream().synchronize()))
+        # the step's launch as shipped (p3d_serve_mse_sync: returns with the results in host memory)
+        out["serve_mse_sync_call"] = med(ss["launch"])
+        args = (h, hx.data_ptr(), 64, hy.data_ptr(), ht.data_ptr(), hl.data_ptr())
+        out["serve_mse_launch_stream_sync"] = med(lambda: (lib.p3d_serve_mse(*args, sh()),
+                                                           torch.cuda.current_stream().synchronize()))
     out["device_ctx"] = med(lambda: torch.cuda.device(model.device).__enter__())
     out["current_stream_sync_call"] = med(lambda: torch.cuda.current_stream(model.device).synchronize())
     ref = model.step(None, x, t, 1.0, isTraining=False)
@@ -117,7 +122,22 @@ def main():
     fl = openpose_frontend.FrameLifter(model, rng2.uniform(200, 600, 64), rng2.uniform(50, 150, 64), use2,
                                        rng2.uniform(-400, 400, 96), rng2.uniform(30, 300, 96), ign3, batch=1)
     e = openpose_frontend.map_frames(rng2.uniform(100, 900, (1, 36)))
-    out["frontend_graph"] = med(lambda: fl.lift_mapped(e))
+    out["frontend_lift_mapped"] = med(lambda: fl.lift_mapped(e))
+    # its pieces: the C call (launch + wait for the completion word), the Python around it, and the
+    # same call on device-resident rows (no PCIe reads / writes inside the kernel)
+    out["frontend_pieces"] = {
+        "lift_sync_call": med(fl._launch),
+        "asarray_store_rows": med(lambda: fl.hin_np.__setitem__(slice(0, 1), np.asarray(e, np.float64))),
+        "out_copy": med(lambda: fl.hout_np[:1].copy()),
+        "stream_handle": med(sh),
+    }
+    dargs = (h, fl.din.data_ptr(), 1, 64, fl.m2.data_ptr(), fl.s2.data_ptr(), fl.u2.data_ptr(), fl.u2.numel(),
+             fl.m3.data_ptr(), fl.s3.data_ptr(), fl.u3.data_ptr(), fl.u3.numel(), 96, fl.p3.data_ptr())
+    out["frontend_pieces"]["lift_sync_device_rows"] = med(lambda: lib.p3d_lift_sync(*dargs, sh()))
+    out["frontend_pieces"]["lift_device_rows_stream_sync"] = med(lambda: (lib.p3d_lift(*dargs, sh()),
+                                                                          torch.cuda.current_stream().synchronize()))
+    raw = rng2.uniform(100, 900, (1, 36))
+    out["frontend_lift_from_openpose_frame"] = med(lambda: fl.lift(raw))
     r_graph = fl.lift_mapped(e)
 
     def eager_lift():
@@ -126,7 +146,7 @@ def main():
         torch.cuda.current_stream().synchronize()
         return fl.hout_np[:1].copy()
     out["frontend_eager_zero_copy"] = med(eager_lift)
-    out["frontend_agree_bitwise"] = bool(np.array_equal(eager_lift(), r_graph))
+    out["frontend_eager_agree_bitwise"] = bool(np.array_equal(eager_lift(), r_graph))
     print(json.dumps(out), flush=True)
     model.close()
 
