@@ -64,6 +64,27 @@ int fail(int code, const std::string& msg) {
 
 int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 
+// Host-side segment timing of serve_impl (dev builds: -DP3D_HOSTPROF; tools/host_prof.sh): per
+// segment the summed steady-clock nanoseconds and count, printed at exit.
+#ifdef P3D_HOSTPROF
+#include <chrono>
+struct HostProf {
+  double ns[16] = {}; long n[16] = {};
+  ~HostProf() {
+    fprintf(stderr, "P3D_HOSTPROF");
+    for (int i = 0; i < 16; ++i) if (n[i]) fprintf(stderr, " s%d=%.3fus", i, ns[i] / n[i] / 1000.0);
+    fprintf(stderr, "\n");
+  }
+};
+static HostProf g_hp;
+#define HP_START auto hp_t = std::chrono::steady_clock::now();
+#define HP(i) do { auto t_ = std::chrono::steady_clock::now(); \
+    g_hp.ns[i] += std::chrono::duration<double, std::nano>(t_ - hp_t).count(); ++g_hp.n[i]; hp_t = t_; } while (0)
+#else
+#define HP_START
+#define HP(i) do { } while (0)
+#endif
+
 struct Tensor {
   std::string name;
   int64_t numel;
@@ -234,6 +255,11 @@ struct p3d_model {
   int serve6_depth = 2;     // k_serve6 weight-ring depth of the 7-tile form (env P3D_SERVE6_DEPTH: 2 or 4)
   int serve6_pair = 1;      // XCD-wide units of 10 row tiles as two 5-row-tile units run side by side (env P3D_SERVE6_PAIR: 0 off)
   std::string serve_kname;  // the kernel the last p3d_serve launched (p3d_kernel_name 3)
+  // the last k_serve6 launch shape, by batch (serve6_plan prices 64 candidates and the kernel name
+  // is a string: both are redone only when the batch changes -- the host enqueue of a serving loop)
+  int64_t s6_B = -1;
+  struct { int S, rt, ncm; bool pair; int depth; } s6_shape{};
+  std::string s6_kname;
   // data-parallel step with the library's own all-reduce (p3d_dp.h)
   p3d_comm* comm = nullptr;      // not owned (p3d_comm_create / p3d_comm_destroy)
   hipStream_t cst = nullptr;     // comm stream (non-blocking), forked from / joined to the caller's stream
@@ -1335,6 +1361,7 @@ static void launch_serve6(const ProfScope& ps, const p3d_model* m, int ncm, int 
 
 static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss,
                       void* stream) {
+  HP_START
   if (!m || !x || !y) return fail(P3D_ERR_ARG, "p3d_serve: null argument");
   const p3d_cfg& c = m->cfg;
   if (B <= 0) return fail(P3D_ERR_ARG, "p3d_serve: batch must be positive");
@@ -1411,26 +1438,44 @@ static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const f
   }
   bool use6 = m->serve6 && c.num_layers > 0 && NDT == 3 && (m->serve6 == 2 || a.nb <= (int64_t)m->serve6_max_nb);
   Serve6Plan plan;
+  int depth = 4;
   if (use6) {
-    plan = serve6_plan(m, B, L / 16);
+    if (B != m->s6_B) {
+      plan = serve6_plan(m, B, L / 16);
+      // the pair form: an XCD-wide unit of 10 row tiles run as two units of 5 side by side, phases
+      // alternating (p3d_serve6.h; the same bits; 20 steps: 99.2 vs 101.1 us, six alternating pairs)
+      if (plan.S > 0 && m->serve6_pair && plan.S == 1 && plan.rt == 10 && L / 64 >= 12) {
+        plan.rt = 5;
+        plan.pair = true;
+      }
+      const int T = L / 16, ncm = plan.ncm;
+      depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
+      if (plan.rt == 2) depth = ncm == 2 ? 4 : 2;
+      if (plan.rt == 1) depth = 4;
+      if (plan.rt > 4) depth = 4;   // (an 8-deep weight ring measured 117 vs 107-112 us at RT = 10)
+      m->s6_shape = {plan.S, plan.rt, plan.ncm, plan.pair, depth};
+      m->s6_kname = plan.S > 0 ? "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ", " +
+                                     std::to_string(plan.rt) + (plan.pair ? ", true>" : ">")
+                               : std::string();
+      m->s6_B = B;
+    }
+    plan.S = m->s6_shape.S; plan.rt = m->s6_shape.rt; plan.ncm = m->s6_shape.ncm; plan.pair = m->s6_shape.pair;
+    depth = m->s6_shape.depth;
     a.split = plan.S;
     use6 = plan.S > 0;                       // no form covers this width: k_serve5
-    // the pair form: an XCD-wide unit of 10 row tiles run as two units of 5 side by side, phases
-    // alternating (p3d_serve6.h; the same bits; 20 steps: 99.2 vs 101.1 us, six alternating pairs)
-    if (use6 && m->serve6_pair && plan.S == 1 && plan.rt == 10 && L / 64 >= 12) {
-      plan.rt = 5;
-      plan.pair = true;
-    }
     if (use6) a.nb = (int)((B + 16 * plan.rt - 1) / (16 * plan.rt));   // units of 16 RT rows
   }
   a.ecg = m->serve_ecg;
   // a HIP graph being captured replays this call with whatever parameters it then finds: the
   // epilogue-constant table is formed inside the graph (one small launch per replay), not
   // decided once at capture time
+  HP(0);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if ((e = hipStreamIsCapturing(st, &cap)) != hipSuccess)
     return fail(P3D_ERR_HIP, std::string("p3d_serve: ") + hipGetErrorString(e));
   const bool capturing = cap != hipStreamCaptureStatusNone;
+  HP(1);
+
   if (use6 && (m->serve_ec_dirty || capturing)) {
     // the epilogue-constant table, formed once per parameter version (refresh_derived, a
     // training forward and every Adam step mark it stale): steady-state calls are one launch
@@ -1457,16 +1502,11 @@ static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const f
   if (use6) {
     a.act = m->serve6_act;                   // [group][4 slabs][16 RT rows][L]; no output partials
     a.part = nullptr;
-    const int T = L / 16;
-    const int ncm = plan.ncm;
-    int depth = ((ncm <= 4 || (ncm == 7 && m->serve6_depth == 4)) && (T / 4) % 4 == 0) ? 4 : 2;
-    if (plan.rt == 2) depth = ncm == 2 ? 4 : 2;
-    if (plan.rt == 1) depth = 4;
-    if (plan.rt > 4) depth = 4;   // (an 8-deep weight ring measured 117 vs 107-112 us at RT = 10)
-    m->serve_kname = "k_serve6<" + std::to_string(depth) + ", 3, " + std::to_string(ncm) + ", " +
-                     std::to_string(plan.rt) + (plan.pair ? ", true>" : ">");
+    if (m->serve_kname != m->s6_kname) m->serve_kname = m->s6_kname;
     ProfScope ps(m, "serve");
-    launch_serve6(ps, m, ncm, depth, plan.rt, plan.pair, (unsigned)m->serve_grid, st, a);
+    HP(2);
+    launch_serve6(ps, m, plan.ncm, depth, plan.rt, plan.pair, (unsigned)m->serve_grid, st, a);
+    HP(3);
   } else {
     m->serve_kname.clear();
     ProfScope ps(m, "serve");
@@ -2197,7 +2237,9 @@ __global__ void k_empty() {}
 extern "C" int p3d_empty_launch(p3d_model* m, int32_t grid, void* stream) {
   if (!m || grid <= 0) return fail(P3D_ERR_ARG, "p3d_empty_launch: bad argument");
   ProfScope ps(m, "empty");
+  HP_START
   go(ps, k_empty, dim3((unsigned)grid), dim3(256), (hipStream_t)stream);
+  HP(8);
   LAUNCH_CHECK("k_empty");
   return P3D_OK;
 }

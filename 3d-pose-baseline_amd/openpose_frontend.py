@@ -21,6 +21,9 @@ import numpy as np
 import data_pipeline as dp
 
 ORDER = [15, 12, 25, 26, 27, 17, 18, 19, 1, 2, 3, 6, 7, 8]   # src/openpose_3dpose_sandbox.py:25
+# the per-joint copies of the mapping as one gather: H3.6M columns 2h, 2h+1 <- OpenPose 2i, 2i+1
+_SRC = np.array([2 * i + k for i in range(len(ORDER)) for k in (0, 1)])
+_DST = np.array([2 * h + k for h in ORDER for k in (0, 1)])
 
 
 def map_frames(frames_xy):
@@ -31,8 +34,7 @@ def map_frames(frames_xy):
     if xy.ndim != 2 or xy.shape[1] < 2 * len(ORDER):
         raise ValueError("expected OpenPose frames [N, >= %d], got %s" % (2 * len(ORDER), xy.shape))
     e = np.zeros((xy.shape[0], 64))
-    for i, h in enumerate(ORDER):
-        e[:, 2 * h:2 * h + 2] = xy[:, 2 * i:2 * i + 2]
+    e[:, _DST] = xy[:, _SRC]
     e[:, 0:2] = (e[:, 2:4] + e[:, 12:14]) / 2            # Hip = mean(RHip, LHip)
     e[:, 28:30] = (e[:, 30:32] + e[:, 24:26]) / 2        # Neck/Nose = mean(Head, Spine)
     e[:, 26:28] = 2 * e[:, 24:26] - e[:, 28:30]          # Thorax = 2 Spine - Neck/Nose
@@ -145,4 +147,6 @@ class FrameLifter:
     def lift(self, frames_xy):
         """OpenPose frames [N, >= 28] -> 3D poses [N, 96] (mm), in calls of `batch` frames."""
         e = map_frames(frames_xy)
+        if e.shape[0] <= self.B:          # (the sandbox's per-frame call: one batch)
+            return self.lift_mapped(e)
         return np.concatenate([self.lift_mapped(e[i:i + self.B]) for i in range(0, e.shape[0], self.B)])

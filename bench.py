@@ -966,10 +966,20 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
     for i in range(n1):
         fl.lift_mapped(e)
     dt = time.perf_counter() - t0
+    raw = rng2.uniform(100, 900, (1, 36))     # an OpenPose frame: the joint mapping included
+    for i in range(20):
+        fl.lift(raw)
+    t0 = time.perf_counter()
+    for i in range(n1):
+        fl.lift(raw)
+    dt_op = time.perf_counter() - t0
     out["frontend_b1"] = {"us_per_frame": round(1e6 * dt / n1, 2), "unit": "us",
-                          "note": "openpose_frontend.FrameLifter: one p3d_lift launch per frame (normalise, "
-                                  "the 6 layers as one persistent k_gemv_chain, unNormalizeData) reading and "
-                                  "writing the pinned frame rows directly + sync"}
+                          "us_per_frame_from_openpose_frame": round(1e6 * dt_op / n1, 2),
+                          "note": "openpose_frontend.FrameLifter.lift_mapped: one p3d_lift_sync call per frame "
+                                  "(normalise, the 6 layers as one persistent k_gemv_chain, unNormalizeData; the "
+                                  "pinned frame rows read and the pinned output rows written by the kernel, which "
+                                  "stores a completion word the host waits on); from_openpose_frame: lift() of a "
+                                  "raw OpenPose frame, the joint mapping included"}
     del fl
     model.close()
     return out

@@ -147,6 +147,27 @@ def main():
         return fl.hout_np[:1].copy()
     out["frontend_eager_zero_copy"] = med(eager_lift)
     out["frontend_eager_agree_bitwise"] = bool(np.array_equal(eager_lift(), r_graph))
+    # host enqueue cost alone (the launch call returns before the kernel runs; synchronize untimed):
+    # the empty kernel, p3d_serve at B = 64 and the headline's 1280 rows, and a trivial ABI call
+    def enq(fn, n=300, warm=30):
+        ts = []
+        for k in range(n + warm):
+            torch.cuda.current_stream().synchronize()
+            t0 = time.perf_counter()
+            fn()
+            if k >= warm:
+                ts.append(time.perf_counter() - t0)
+        torch.cuda.current_stream().synchronize()
+        ts.sort()
+        return round(1e6 * ts[len(ts) // 2], 2)
+    import ctypes
+    flg = ctypes.c_int32()
+    x1280 = torch.zeros((1280, 32), dtype=f32, device="cuda")
+    y1280 = torch.empty((1280, 48), dtype=f32, device="cuda")
+    out["enqueue"] = {"empty_kernel": enq(lambda: lib.p3d_empty_launch(h, 256, sh())),
+                      "serve_b64": enq(model.serve_launcher(dx, dy)),
+                      "serve_b1280": enq(model.serve_launcher(x1280, y1280)),
+                      "abi_call_no_launch": enq(lambda: lib.p3d_error_flags(h, ctypes.byref(flg), 0))}
     print(json.dumps(out), flush=True)
     model.close()
 
