@@ -2445,7 +2445,13 @@ static int host_finish(p3d_model* m, int rc, unsigned seq, hipStream_t st, const
     const hipError_t e = hipStreamSynchronize(st);
     return e == hipSuccess ? P3D_OK : fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   }
-  return host_wait(m, seq, st, what);
+  if (int rc2 = host_wait(m, seq, st, what)) return rc2;
+  // the kernels' pinned error words, read here so that the caller's separate check is needed only
+  // when this call fails (p3d_error_flags reports and clears them)
+  if (__atomic_load_n(&m->errw[0], __ATOMIC_ACQUIRE) || __atomic_load_n(&m->errw[1], __ATOMIC_ACQUIRE))
+    return fail(P3D_ERR_HIP, std::string(what) + ": a kernel reported a failed in-launch synchronisation "
+                                                 "(p3d_error_flags)");
+  return P3D_OK;
 }
 
 // (include/p3d.h) p3d_serve_mse, returning once y and *loss hold the results

@@ -899,10 +899,12 @@ class LinearModel(object):
                 np.copyto(ss["ht_np"], t, casting="unsafe")
                 rc = ss["launch"]()
                 if rc:
+                    self.check_errors()           # (raises with the kernels' own report, if any)
                     check(rc, "p3d_serve_mse")
                 if ss["sync"]:
                     self.torch.cuda.current_stream(self.device).synchronize()
-                self.check_errors()
+                    self.check_errors()
+                # (p3d_serve_mse_sync read the error words itself: it returns nonzero when one is set)
                 lv = float(ss["hl_np"][0])
                 return lv, Summary("loss/loss", lv), ss["hy_np"].copy()
         st = self._host_step_state(training, B, keep)

@@ -136,6 +136,7 @@ class FrameLifter:
             rc = self._launch()
             if rc:
                 import _p3d
+                self.model.check_errors()         # (raises with the kernels' own report, if any)
                 _p3d.check(rc, "p3d_lift")
             if not self._host_wait:
                 self.torch.cuda.current_stream(self.model.device).synchronize()

@@ -147,7 +147,8 @@ int p3d_serve_mse(p3d_model* m, const float* x, int64_t B, float* y, const float
  * the loss are system-visible, and the host waits on that word rather than on the runtime's
  * completion signal; the stream itself is not synchronised (later work on it is ordered behind the
  * launch).  Not capturable (P3D_ERR_STATE on a capturing stream).  Errors as p3d_serve_mse, plus
- * P3D_ERR_HIP when the launch ends without storing the word. */
+ * P3D_ERR_HIP when the launch ends without storing the word or when a kernel's error word is set
+ * (p3d_error_flags reports which). */
 int p3d_serve_mse_sync(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss, void* stream);
 /* 0 if every p3d_serve launch so far completed its synchronisation (synchronises the device,
  * then reads the kernels' pinned error word).  After a failure p3d_serve refuses new launches

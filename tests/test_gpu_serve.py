@@ -517,3 +517,21 @@ def test_step_eval_host_wait_equals_stream_sync(monkeypatch):
     for (la, _, ya), (lb, _, yb) in zip(res["1"], res["0"]):
         assert la == lb
         np.testing.assert_array_equal(ya, yb)
+
+
+def test_step_eval_reports_a_failed_launch(monkeypatch):
+    """The eval step's one launch (p3d_serve_mse_sync) on a model whose serve launches fail their
+    placement (test hook P3D_SERVE_TEST_FAULT): step() raises -- the sync call reads the kernels'
+    error words after its wait and fails, and the host names the failure -- instead of returning
+    the launch's NaN rows as a result."""
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    monkeypatch.setenv("P3D_SERVE_TEST_FAULT", "1")
+    st, m = make(cfg)
+    monkeypatch.delenv("P3D_SERVE_TEST_FAULT")
+    rng = np.random.default_rng(4)
+    x, t = rng.standard_normal((64, 32)), rng.standard_normal((64, 48))
+    with pytest.raises(_p3d.P3DError):
+        m.step(None, x, t, 1.0, isTraining=False)
+    torch.cuda.synchronize()
+    m.close()
