@@ -81,6 +81,10 @@ SIGNATURES = [
     ("p3d_stream_wait_grad", c_int32, [c_void_p, c_int32, c_void_p]),
     ("p3d_profile_start", c_int32, [c_void_p, c_int32]),
     ("p3d_empty_launch", c_int32, [c_void_p, c_int32, c_void_p]),
+    ("p3d_host_signal", c_int32, [c_void_p, c_void_p]),
+    ("p3d_host_wait", c_int32, [c_void_p, c_uint32, c_void_p]),
+    ("p3d_host_alloc", c_void_p, [c_int64]),
+    ("p3d_host_free", c_int32, [c_void_p]),
     ("p3d_profile_stop", c_int32, [c_void_p, c_char_p, c_int64]),
     ("p3d_time_layer", c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p]),
     ("p3d_cam_transform", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),

@@ -2404,8 +2404,17 @@ extern "C" int p3d_lift(p3d_model* m, const double* raw, int64_t B, int32_t D2, 
 // the stream is queried, so a launch that ends without storing the word (a fault, a launch whose
 // workgroups could not synchronise) is reported instead of waited for.  The stream's own completion
 // is not waited for: later work on it is ordered behind the launch as usual.
-static int host_wait(p3d_model* m, unsigned seq, hipStream_t st, const char* what) {
-  unsigned* word = reinterpret_cast<unsigned*>(m->errw) + 8;
+// the kernels' pinned error words, read after a host wait so that the caller's separate check is
+// needed only when the call fails (p3d_error_flags reports and clears them)
+static int host_errors(p3d_model* m, const char* what) {
+  if (__atomic_load_n(&m->errw[0], __ATOMIC_ACQUIRE) || __atomic_load_n(&m->errw[1], __ATOMIC_ACQUIRE))
+    return fail(P3D_ERR_HIP, std::string(what) + ": a kernel reported a failed in-launch synchronisation "
+                                                 "(p3d_error_flags)");
+  return P3D_OK;
+}
+
+static int host_wait(p3d_model* m, unsigned seq, hipStream_t st, const char* what, int idx = 8) {
+  unsigned* word = reinterpret_cast<unsigned*>(m->errw) + idx;
   for (uint64_t n = 1;; ++n) {
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return P3D_OK;
     if ((n & 4095) == 0) {
@@ -2446,12 +2455,7 @@ static int host_finish(p3d_model* m, int rc, unsigned seq, hipStream_t st, const
     return e == hipSuccess ? P3D_OK : fail(P3D_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   }
   if (int rc2 = host_wait(m, seq, st, what)) return rc2;
-  // the kernels' pinned error words, read here so that the caller's separate check is needed only
-  // when this call fails (p3d_error_flags reports and clears them)
-  if (__atomic_load_n(&m->errw[0], __ATOMIC_ACQUIRE) || __atomic_load_n(&m->errw[1], __ATOMIC_ACQUIRE))
-    return fail(P3D_ERR_HIP, std::string(what) + ": a kernel reported a failed in-launch synchronisation "
-                                                 "(p3d_error_flags)");
-  return P3D_OK;
+  return host_errors(m, what);
 }
 
 // (include/p3d.h) p3d_serve_mse, returning once y and *loss hold the results
@@ -2475,6 +2479,50 @@ extern "C" int p3d_lift_sync(p3d_model* m, const double* raw, int64_t B, int32_t
   if (int rc = host_arm(m, st, "p3d_lift_sync", seq)) return rc;
   return host_finish(m, p3d_lift(m, raw, B, D2, mean2, std2, use2, U2, mean3, std3, use3, U3, D3, out, stream), seq, st,
                      "p3d_lift_sync");
+}
+
+// One workgroup, stream-ordered behind everything before it (a captured step's last node): the
+// model's signal counter advanced and its new value stored into the pinned word errw[9] with a
+// system-scope release.  The earlier kernels' host-memory outputs must be in coherent host memory
+// (p3d_host_alloc: uncached on the device, complete when their kernels complete).
+__global__ void k_host_signal(unsigned* cnt, unsigned* word) {
+  if (threadIdx.x == 0) {
+    const unsigned v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(cnt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// (include/p3d.h) enqueue the signal; capturable (each replay of a graph holding it signals once)
+extern "C" int p3d_host_signal(p3d_model* m, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_host_signal: null model");
+  k_host_signal<<<1, 64, 0, (hipStream_t)stream>>>(m->hcnt + 8, reinterpret_cast<unsigned*>(m->hflag_dev) + 1);
+  LAUNCH_CHECK("k_host_signal");
+  return P3D_OK;
+}
+
+// (include/p3d.h) wait on the host until the model's signal count reaches `count`, then read the
+// kernels' error words (the stream is queried every 4096 polls, as the *_sync calls do)
+extern "C" int p3d_host_wait(p3d_model* m, uint32_t count, void* stream) {
+  if (!m) return fail(P3D_ERR_ARG, "p3d_host_wait: null model");
+  if (int rc = host_wait(m, count, (hipStream_t)stream, "p3d_host_wait", 9)) return rc;
+  return host_errors(m, "p3d_host_wait");
+}
+
+// (include/p3d.h) coherent pinned host memory the kernels write without caching it on the device
+extern "C" void* p3d_host_alloc(int64_t bytes) {
+  void* p = nullptr;
+  if (bytes <= 0) { fail(P3D_ERR_ARG, "p3d_host_alloc: bytes must be positive"); return nullptr; }
+  const hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) { fail(P3D_ERR_HIP, std::string("p3d_host_alloc: ") + hipGetErrorString(e)); return nullptr; }
+  memset(p, 0, (size_t)bytes);
+  return p;
+}
+
+extern "C" int p3d_host_free(void* p) {
+  if (!p) return P3D_OK;
+  const hipError_t e = hipHostFree(p);
+  return e == hipSuccess ? P3D_OK : fail(P3D_ERR_HIP, std::string("p3d_host_free: ") + hipGetErrorString(e));
 }
 
 extern "C" int64_t p3d_moments_workspace(int64_t F, int32_t D) {

@@ -193,6 +193,31 @@ class _FlatViews(dict):
         return dict.__getitem__(self, key)
 
 
+class _HostBuf:
+    """Coherent pinned host memory from the library (p3d_host_alloc: mapped, not cached on the
+    device), freed with the object; kernels write their host-memory outputs here when the host
+    waits on a signal word rather than on the stream (p3d_host_wait)."""
+
+    def __init__(self, nbytes):
+        self.ptr = lib().p3d_host_alloc(int(nbytes))
+        if not self.ptr:
+            raise _p3d.P3DError("p3d_host_alloc: %s" % lib().p3d_last_error().decode())
+        self.nbytes = int(nbytes)
+
+    def floats(self, n):
+        import ctypes
+        assert 4 * n <= self.nbytes
+        return np.ctypeslib.as_array((ctypes.c_float * n).from_address(self.ptr))
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().p3d_host_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
 class LinearModel(object):
     """A simple Linear+RELU model (src/linear_model.py:31), on MI355X HIP kernels."""
 
@@ -265,6 +290,7 @@ class LinearModel(object):
         self._step_host = 0   # host mirror of the device global_step (step() summaries, no sync)
         self._host_steps = {}  # step() staging buffers / eval graphs per (mode, B, keep)
         self._serve_steps = {}  # step(isTraining=False) one-launch states per batch (p3d_serve_mse)
+        self._hsig = 0          # signals the captured training steps have been replayed with (p3d_host_signal)
         self._dy = torch.empty((self.max_batch, self.output_size), dtype=torch.float32, device=self.device)
         if init:
             self.initialize(self.seed)
@@ -788,6 +814,9 @@ class LinearModel(object):
         if st is not None:
             return st
         while len(self._host_steps) >= 8:
+            # (a replay may still be finishing its last node: a step waited on its signal word, not
+            # on the stream -- the evicted graph and its buffers go only after the device is done)
+            torch.cuda.synchronize(self.device)
             self._host_steps.pop(next(iter(self._host_steps)))
         f32 = torch.float32
         nx, nt, ny = B * self.input_size, B * self.output_size, B * self.output_size
@@ -821,19 +850,48 @@ class LinearModel(object):
             with torch.cuda.graph(g, stream=side):
                 body()
             st["graph"] = g
-        elif not self.data_parallel and os.environ.get("P3D_STEP_GRAPH", "1") != "0":
-            def body():
-                st["din"].copy_(st["hin"], non_blocking=True)
-                self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"], loss_out=st["dl"])
-                st["hout"].copy_(st["dout"], non_blocking=True)
-            side = torch.cuda.Stream(self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
-            g = torch.cuda.CUDAGraph()
-            # captured, not run (a training step has side effects): no eager warm-up
-            with torch.cuda.graph(g, stream=side):
-                body()
-            self._step_host -= 1            # the capture issued no step
-            st["graph"] = g
+        elif not self.data_parallel and (os.environ.get("P3D_STEP_GRAPH", "1") != "0" or
+                                         os.environ.get("P3D_HOST_WAIT", "1") != "0"):
+            signal = os.environ.get("P3D_HOST_WAIT", "1") != "0"
+            eager = os.environ.get("P3D_STEP_GRAPH", "1") == "0"
+            if signal:
+                # round 6: the step's kernels read x / t from the pinned block and write y and the
+                # loss into coherent host memory (p3d_host_alloc), and the graph ends with
+                # p3d_host_signal -- no copy nodes, and step() waits on the signal word instead of the
+                # runtime's completion signal (P3D_HOST_WAIT=0: the copy-node graph + a synchronize)
+                import ctypes
+                hb = _HostBuf(4 * (ny + 4))
+                hv = hb.floats(ny + 4)
+                st["hbuf"] = hb
+                st["hy_np"], st["hl_np"] = hv[:ny].reshape(B, self.output_size), hv[ny:ny + 1]
+                h, c = self._h, ctypes.c_void_p
+                px, pt = c(hin.data_ptr()), c(hin.data_ptr() + 4 * nx)
+                py, pl = c(hb.ptr), c(hb.ptr + 4 * ny)
+
+                def body():
+                    sh = c(_p3d.stream_handle())
+                    self._x_keep = st["hx"]     # (the backward differentiates the x buffer)
+                    check(lib().p3d_train_step(h, px, pt, B, py, float(keep), self.seed, self.lr0, 100000.0, 0.96,
+                                               pl, sh), "p3d_train_step")
+                    check(lib().p3d_host_signal(h, sh), "p3d_host_signal")
+            else:
+                def body():
+                    st["din"].copy_(st["hin"], non_blocking=True)
+                    self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"], loss_out=st["dl"])
+                    st["hout"].copy_(st["dout"], non_blocking=True)
+            st["signal"] = signal
+            if eager:                       # (P3D_STEP_GRAPH=0 with the signal: the same calls, issued each step)
+                st["run"] = body
+            else:
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                g = torch.cuda.CUDAGraph()
+                # captured, not run (a training step has side effects): no eager warm-up
+                with torch.cuda.graph(g, stream=side):
+                    body()
+                if not signal:
+                    self._step_host -= 1    # the capture issued no step (train_step_device counts one)
+                st["graph"] = g
         self._host_steps[key] = st
         return st
 
@@ -911,20 +969,31 @@ class LinearModel(object):
         np.copyto(st["hx_np"], x, casting="unsafe")     # float64 -> float32, as the placeholders cast
         np.copyto(st["ht_np"], t, casting="unsafe")
         stream = self.torch.cuda.current_stream(self.device)
-        if st["graph"] is not None:
-            if training:
-                lr = exponential_decay(self.lr0, self._step_host)
+        if training:
+            lr = exponential_decay(self.lr0, self._step_host)
+        if st.get("run") is not None:               # the zero-copy step issued eagerly + its signal
+            st["run"]()
+            self._step_host += 1
+        elif st["graph"] is not None:
             st["graph"].replay()
             if training:
                 self._step_host += 1
                 check(lib().p3d_params_changed(self._h), "p3d_params_changed")
         else:
-            lr = exponential_decay(self.lr0, self._step_host)
             st["din"].copy_(st["hin"], non_blocking=True)
             self.train_step_device(st["dx"], st["dt"], keep, out=st["dy"], loss_out=st["dl"])
             st["hout"].copy_(st["dout"], non_blocking=True)
-        stream.synchronize()
-        self.check_errors()
+        if st.get("signal"):
+            # the step's last launch signals once per step: wait on that, not on the stream (it
+            # reads the kernels' error words too)
+            self._hsig = (self._hsig + 1) & 0xffffffff
+            rc = lib().p3d_host_wait(self._h, self._hsig, _p3d.stream_handle())
+            if rc:
+                self.check_errors()           # (raises with the kernels' own report, if any)
+                check(rc, "p3d_host_wait")
+        else:
+            stream.synchronize()
+            self.check_errors()
         lv = float(st["hl_np"][0])
         out = st["hy_np"].copy()
         if training:

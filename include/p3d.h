@@ -334,6 +334,22 @@ int p3d_profile_stop(p3d_model* m, char* out, int64_t out_len);
  * the model's kernels (with the model's event pair while p3d_profile_start is active). */
 int p3d_empty_launch(p3d_model* m, int32_t grid, void* stream);
 
+/* Completion of a captured sequence without the runtime's completion signal (the reference's
+ * session.run returns its fetches; LinearModel.step(isTraining=True) from numpy): p3d_host_signal
+ * enqueues one small kernel that advances the model's signal counter and stores the new count into
+ * a pinned word (system-scope release); it is capturable, and each replay of a graph holding it
+ * signals once.  p3d_host_wait(m, count, stream) returns once the count has reached `count` -- the
+ * kernels before the signal have completed and their writes to coherent host memory are visible --
+ * then reports a set kernel error word as P3D_ERR_HIP (p3d_error_flags says which); it polls the
+ * stream now and then, so a failed launch is reported instead of waited for.  The stream itself
+ * is not synchronised.  p3d_host_alloc / p3d_host_free: coherent pinned host memory (mapped, not
+ * cached on the device), where kernels' host-memory outputs must live for p3d_host_wait to cover
+ * them. */
+int p3d_host_signal(p3d_model* m, void* stream);
+int p3d_host_wait(p3d_model* m, uint32_t count, void* stream);
+void* p3d_host_alloc(int64_t bytes);
+int p3d_host_free(void* p);
+
 /* Roofline timing hook: `reps` back-to-back launches of hidden layer `layer`
  * (1 .. 2*num_layers) of the inference forward over workspace rows [0, B). */
 int p3d_time_layer(p3d_model* m, int32_t layer, int64_t B, int32_t reps, void* stream);

@@ -708,28 +708,40 @@ def test_wgrad_multi_bit_identical(max_norm, p14, B, monkeypatch):
     assert torch.equal(gs[0], gs[1])
 
 
-def test_step_training_graph_bit_identical_to_eager(monkeypatch):
+@pytest.mark.parametrize("B", [64, 17])
+def test_step_training_graph_bit_identical_to_eager(monkeypatch, B):
     """LinearModel.step(isTraining=True) from numpy replays a cached HIP graph of the whole
-    training step (H2D, forward, MSE, backward, fused Adam, D2H); the same steps issued eagerly
-    (P3D_STEP_GRAPH=0) give the same bits: outputs, losses, weights, Adam slots, step state,
-    learning-rate summaries."""
+    training step: by default (round 6) the kernels read x / t from the pinned block and write y /
+    the loss into coherent host memory, and the graph ends with p3d_host_signal, which step() waits
+    on (no copy nodes, no stream synchronize); P3D_HOST_WAIT=0 keeps the copy-node graph (H2D,
+    forward, MSE, backward, fused Adam, D2H) + a synchronize; P3D_STEP_GRAPH=0 issues the same
+    calls eagerly each step (with or without the signal).  All four give the same bits: outputs,
+    losses, weights, Adam slots, step state, learning-rate summaries -- 6 steps on fresh batches,
+    each read straight after its call, so a result of the previous step would show."""
     cfg = ref_mlp.Cfg(linear_size=256, num_layers=2, residual=True, batch_norm=True)
     rng = np.random.default_rng(77)
-    batches = [(rng.standard_normal((64, 32)), rng.standard_normal((64, 48))) for _ in range(6)]
+    batches = [(rng.standard_normal((B, 32)), rng.standard_normal((B, 48))) for _ in range(6)]
     runs = {}
-    for mode in ("1", "0"):
+    for mode, hw in (("1", "1"), ("1", "0"), ("0", "1"), ("0", "0")):
         monkeypatch.setenv("P3D_STEP_GRAPH", mode)
-        st, m = make(cfg, lr=1e-3)
+        monkeypatch.setenv("P3D_HOST_WAIT", hw)
+        st, m = make(cfg, lr=1e-3, max_batch=64)
         res = [m.step(None, x, t, 0.5, isTraining=True) for x, t in batches]
-        runs[mode] = (res, m.get_state(), m.get_step(), m._step_host)
+        runs[mode + hw] = (res, m.get_state(), m.get_step(), m._step_host)
+        sst = m._host_steps[(True, B, 0.5, m.lr0, m.seed)]
+        assert bool(sst.get("signal")) == (hw == "1") and (sst.get("run") is not None) == (mode + hw == "01")
         m.close()
-    (ra, sa, ga, ha), (rb, sb, gb, hb) = runs["1"], runs["0"]
-    assert ga == gb and ha == hb == 6
-    for (la, _, lra, oa), (lb, _, lrb, ob) in zip(ra, rb):
-        assert la == lb and lra.value == lrb.value
-        np.testing.assert_array_equal(oa, ob)
-    for k in sa:
-        np.testing.assert_array_equal(np.asarray(sa[k]), np.asarray(sb[k]), err_msg=k)
+    ra, sa, ga, ha = runs["11"]
+    assert ha == 6
+    for k in ("10", "01", "00"):
+        rb, sb, gb, hb = runs[k]
+        assert ga == gb and hb == 6
+        for (la, _, lra, oa), (lb, _, lrb, ob) in zip(ra, rb):
+            assert la == lb and lra.value == lrb.value
+            np.testing.assert_array_equal(oa, ob)
+        for n in sa:
+            np.testing.assert_array_equal(np.asarray(sa[n]), np.asarray(sb[n]), err_msg=n)
+    assert ra[0][0] != ra[1][0]
 
 
 @pytest.mark.parametrize("dp", [False, True])

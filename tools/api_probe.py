@@ -168,6 +168,33 @@ def main():
                       "serve_b64": enq(model.serve_launcher(dx, dy)),
                       "serve_b1280": enq(model.serve_launcher(x1280, y1280)),
                       "abi_call_no_launch": enq(lambda: lib.p3d_error_flags(h, ctypes.byref(flg), 0))}
+    # the training step from numpy (the captured step without copy nodes, waited on its signal word)
+    xtr, ttr = rng.standard_normal((64, 32)), rng.standard_normal((64, 48))
+    out["step_train_b64"] = med(lambda: model.step(None, xtr, ttr, 0.5, isTraining=True), n=200, warm=20)
+    sttr = model._host_step_state(True, 64, 0.5)
+    if sttr.get("signal"):
+        def replay_then_wait(timed):
+            t0 = time.perf_counter()
+            sttr["graph"].replay()
+            t1 = time.perf_counter()
+            model._hsig = (model._hsig + 1) & 0xffffffff
+            _p3d.check(lib.p3d_host_wait(h, model._hsig, sh()), "p3d_host_wait")
+            t2 = time.perf_counter()
+            model._step_host += 1
+            timed.append((t1 - t0, t2 - t0))
+        tt = []
+        for _ in range(220):
+            replay_then_wait(tt)
+        tt = tt[20:]
+        out["train_pieces"] = {"graph_replay_call": round(1e6 * sorted(a for a, _ in tt)[len(tt) // 2], 2),
+                               "replay_to_signal": round(1e6 * sorted(b for _, b in tt)[len(tt) // 2], 2),
+                               "params_changed": med(lambda: lib.p3d_params_changed(h))}
+    # the same step's calls issued eagerly each step (P3D_STEP_GRAPH=0), with the signal
+    os.environ["P3D_STEP_GRAPH"] = "0"
+    torch.cuda.synchronize()
+    model._host_steps.clear()
+    out["step_train_b64_eager_signal"] = med(lambda: model.step(None, xtr, ttr, 0.5, isTraining=True), n=200, warm=20)
+    del os.environ["P3D_STEP_GRAPH"]
     print(json.dumps(out), flush=True)
     model.close()
 
