@@ -897,6 +897,13 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
         barrier_sync(world)
         dt = max_over_ranks(time.perf_counter() - t0, world)
         out[name] = {"value": round(world * n * BATCH / dt, 1), "unit": "poses/s", "ms_per_step": round(1000.0 * dt / n, 4)}
+    out["eval"]["note"] = ("one p3d_serve_mse_sync call per step: the kernel reads x / t from pinned memory, writes y and the "
+                           "fused loss there and stores a completion word the host waits on")
+    out["train"]["note"] = ("one step: %s" % ("the data-parallel step (eager, RCCL all-reduce), a stream synchronize"
+                                               if world > 1 else
+                                               "the captured step (x / t read from pinned memory, y / loss written to "
+                                               "coherent host memory) replayed, its last node a host signal the host "
+                                               "waits on"))
     # the OpenPose front end's per-frame call (src/openpose_3dpose_sandbox.py:317-356): B = 1
     x1, t1 = xs[0][:1], np.zeros((1, OUT))
     for i in range(20):
