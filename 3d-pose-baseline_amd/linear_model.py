@@ -835,21 +835,47 @@ class LinearModel(object):
         st["hx_np"], st["ht_np"] = st["hx"].numpy(), st["ht"].numpy()
         st["hy_np"], st["hl_np"] = st["hy"].numpy(), st["hl"].numpy()
         if not training:
-            def body():
-                st["din"].copy_(st["hin"], non_blocking=True)
-                self.forward_device(st["dx"], False, keep, out=st["dy"])
-                check(lib().p3d_mse(ptr(st["dy"]), ptr(st["dt"]), B, self.output_size, ptr(st["dl"]), 0,
-                                    self.stream()), "p3d_mse")
-                st["hout"].copy_(st["dout"], non_blocking=True)
+            # (batches the one-launch p3d_serve_mse_sync path does not take: B <= 4, B > 2048, bf16)
+            signal = os.environ.get("P3D_HOST_WAIT", "1") != "0"
+            if signal:
+                # round 6: the forward reads x from the pinned block and writes y into coherent host
+                # memory, p3d_mse reads them there and writes the loss beside y, and the graph ends with
+                # p3d_host_signal -- no copy nodes, and step() waits on the signal word
+                import ctypes
+                hb = _HostBuf(4 * (ny + 4))
+                hv = hb.floats(ny + 4)
+                st["hbuf"] = hb
+                st["hy_np"], st["hl_np"] = hv[:ny].reshape(B, self.output_size), hv[ny:ny + 1]
+                h, c = self._h, ctypes.c_void_p
+                px, pt = c(hin.data_ptr()), c(hin.data_ptr() + 4 * nx)
+                py, pl = c(hb.ptr), c(hb.ptr + 4 * ny)
+
+                def body():
+                    sh = c(_p3d.stream_handle())
+                    check(lib().p3d_forward_ex(h, px, B, py, 0, float(keep), self.seed, 0, self.rank * B, 0, sh),
+                          "p3d_forward")
+                    check(lib().p3d_mse(py, pt, B, self.output_size, pl, None, sh), "p3d_mse")
+                    check(lib().p3d_host_signal(h, sh), "p3d_host_signal")
+            else:
+                def body():
+                    st["din"].copy_(st["hin"], non_blocking=True)
+                    self.forward_device(st["dx"], False, keep, out=st["dy"])
+                    check(lib().p3d_mse(ptr(st["dy"]), ptr(st["dt"]), B, self.output_size, ptr(st["dl"]), 0,
+                                        self.stream()), "p3d_mse")
+                    st["hout"].copy_(st["dout"], non_blocking=True)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
                 body()                      # eager warm-up (evaluation has no side effects)
             torch.cuda.current_stream(self.device).wait_stream(side)
+            if signal:                      # (the warm-up signalled once)
+                torch.cuda.synchronize(self.device)
+                self._hsig = (self._hsig + 1) & 0xffffffff
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=side):
                 body()
             st["graph"] = g
+            st["signal"] = signal
         elif not self.data_parallel and (os.environ.get("P3D_STEP_GRAPH", "1") != "0" or
                                          os.environ.get("P3D_HOST_WAIT", "1") != "0"):
             signal = os.environ.get("P3D_HOST_WAIT", "1") != "0"

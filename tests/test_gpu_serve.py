@@ -500,23 +500,33 @@ def test_serve_mse_sync_returns_with_results_in_host_memory(B):
     m.close()
 
 
-def test_step_eval_host_wait_equals_stream_sync(monkeypatch):
-    """LinearModel.step(isTraining=False) at B = 64 through p3d_serve_mse_sync (default) and through
-    p3d_serve_mse + a stream synchronize (P3D_HOST_WAIT=0): 10 steps on fresh inputs, the same
-    outputs and loss bit for bit, step by step."""
+@pytest.mark.parametrize("B", [64, 3])
+def test_step_eval_host_wait_equals_stream_sync(monkeypatch, B):
+    """LinearModel.step(isTraining=False) through the host-wait forms (default) and through the
+    stream-synchronised ones (P3D_HOST_WAIT=0): B = 64 is one p3d_serve_mse_sync call vs
+    p3d_serve_mse + a synchronize; B = 3 (the batch <= 4 chain) is the captured forward + MSE whose
+    last node is p3d_host_signal, reading x / t from pinned memory and writing y / the loss into
+    coherent host memory, vs the copy-node graph + a synchronize.  10 steps on fresh inputs, the
+    same outputs and loss bit for bit, step by step, and the oracle's eval step."""
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     res = {}
     for hw in ("1", "0"):
         monkeypatch.setenv("P3D_HOST_WAIT", hw)
         st, m = make(cfg)
         rng = np.random.default_rng(77)
-        res[hw] = [m.step(None, rng.standard_normal((64, 32)), rng.standard_normal((64, 48)), 1.0, isTraining=False)
-                   for _ in range(10)]
-        assert m._serve_steps[64]["sync"] == (hw == "0")
+        xs = [(rng.standard_normal((B, 32)), rng.standard_normal((B, 48))) for _ in range(10)]
+        res[hw] = [m.step(None, x, t, 1.0, isTraining=False) for x, t in xs]
+        if B == 64:
+            assert m._serve_steps[64]["sync"] == (hw == "0")
+        else:
+            assert bool(m._host_steps[(False, B, 1.0, m.lr0, m.seed)].get("signal")) == (hw == "1")
         m.close()
     for (la, _, ya), (lb, _, yb) in zip(res["1"], res["0"]):
         assert la == lb
         np.testing.assert_array_equal(ya, yb)
+    rl, ro = ref_mlp.eval_step(st, xs[-1][0], xs[-1][1])
+    close(res["1"][-1][2], ro)
+    assert abs(res["1"][-1][0] - rl) <= 1e-5 * max(1.0, abs(rl))
 
 
 def test_step_eval_reports_a_failed_launch(monkeypatch):
