@@ -44,9 +44,15 @@ def main():
     out = {}
     out["step_eval_b64"] = med(lambda: model.step(None, x, t, 1.0, isTraining=False))
     st = model._host_step_state(False, 64, 1.0)
+
+    def replay_sync(st_):
+        st_["graph"].replay()
+        if st_.get("signal"):     # (a graph ending in p3d_host_signal: keep the model's count in step)
+            model._hsig = (model._hsig + 1) & 0xffffffff
+        torch.cuda.current_stream().synchronize()
     out["pieces"] = {
         "copyto_x_t": med(lambda: (np.copyto(st["hx_np"], x, casting="unsafe"), np.copyto(st["ht_np"], t, casting="unsafe"))),
-        "graph_replay_sync": med(lambda: (st["graph"].replay(), torch.cuda.current_stream().synchronize())),
+        "graph_replay_sync": med(lambda: replay_sync(st)),
         "check_errors": med(model.check_errors),
         "out_copy": med(lambda: st["hy_np"].copy()),
         "sync_idle": med(lambda: torch.cuda.current_stream().synchronize()),
@@ -119,8 +125,9 @@ def main():
     rng2 = np.random.default_rng(600)
     use2, _ = data_utils.dimension_sets(2)
     _, ign3 = data_utils.dimension_sets(3)
-    fl = openpose_frontend.FrameLifter(model, rng2.uniform(200, 600, 64), rng2.uniform(50, 150, 64), use2,
-                                       rng2.uniform(-400, 400, 96), rng2.uniform(30, 300, 96), ign3, batch=1)
+    stats = (rng2.uniform(200, 600, 64), rng2.uniform(50, 150, 64), use2, rng2.uniform(-400, 400, 96),
+             rng2.uniform(30, 300, 96), ign3)
+    fl = openpose_frontend.FrameLifter(model, *stats, batch=1)
     e = openpose_frontend.map_frames(rng2.uniform(100, 900, (1, 36)))
     out["frontend_lift_mapped"] = med(lambda: fl.lift_mapped(e))
     # its pieces: the C call (launch + wait for the completion word), the Python around it, and the
