@@ -545,3 +545,37 @@ def test_step_eval_reports_a_failed_launch(monkeypatch):
         m.step(None, x, t, 1.0, isTraining=False)
     torch.cuda.synchronize()
     m.close()
+
+
+def test_host_wait_reports_instead_of_spinning():
+    """p3d_host_wait / the *_sync calls never spin on a word nothing will store: waiting for a
+    signal count no launch was issued for returns P3D_ERR_HIP once the stream reports idle; a
+    signal then a wait for its count returns at once; p3d_serve_mse_sync on a capturing stream is
+    refused (P3D_ERR_STATE) before anything is launched."""
+    import ctypes
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=256, num_layers=1, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    lib = _p3d.lib()
+    sh = ctypes.c_void_p(_p3d.stream_handle())
+    torch.cuda.synchronize()
+    rc = lib.p3d_host_wait(m._h, (m._hsig + 5) & 0xffffffff, sh)
+    assert rc == 2 and b"without storing" in lib.p3d_last_error()
+    _p3d.check(lib.p3d_host_signal(m._h, sh), "p3d_host_signal")
+    m._hsig = (m._hsig + 1) & 0xffffffff
+    _p3d.check(lib.p3d_host_wait(m._h, m._hsig, sh), "p3d_host_wait")
+    # refused inside a capture, nothing launched (the capture then ends empty)
+    hx = torch.zeros((64, 32)).pin_memory()
+    ht = torch.zeros((64, 48)).pin_memory()
+    hy = torch.empty((64, 48)).pin_memory()
+    hl = torch.zeros(4).pin_memory()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rc = lib.p3d_serve_mse_sync(m._h, ctypes.c_void_p(hx.data_ptr()), 64, ctypes.c_void_p(hy.data_ptr()),
+                                    ctypes.c_void_p(ht.data_ptr()), ctypes.c_void_p(hl.data_ptr()),
+                                    ctypes.c_void_p(_p3d.stream_handle()))
+    assert rc == 3, rc
+    torch.cuda.synchronize()
+    m.check_errors()
+    m.close()
