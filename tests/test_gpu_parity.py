@@ -686,6 +686,15 @@ def test_bf16_inference_matches_emulated_oracle(L, N, B):
     assert np.abs(y - ref32).mean() <= 0.05 * np.abs(ref32).mean()
     with pytest.raises(ValueError):
         m.forward_device(torch.from_numpy(x).cuda(), training=True)
+    # the reference's eval step() on the bf16 model (the captured forward + MSE ending in a host
+    # signal, inputs read from pinned memory, outputs written to coherent host memory): the same
+    # outputs bit for bit, the MSE of them
+    t = np.random.default_rng(B + 1).standard_normal((B, 48)).astype(np.float32)
+    for _ in range(2):
+        loss, _, ys = m.step(None, x.astype(np.float64), t.astype(np.float64), 1.0, isTraining=False)
+        np.testing.assert_array_equal(ys, y)
+        rl = float(np.mean((y.astype(np.float64) - t) ** 2))
+        assert abs(loss - rl) <= 1e-5 * max(1.0, rl), (loss, rl)
     m.close()
 
 
