@@ -292,6 +292,49 @@ __device__ __forceinline__ float p3d_gemv_in_value_n(const GemvArgs& in, const G
   }
   return p3d_gemv_epi(in, e, zs, r, f);
 }
+// The raw rows normalised into LDS by one wave, lane d taking column d of every row (D2 <= 64):
+// the rows, the statistics and (separately, scalar) the used-column indices are requested in one
+// round, so the indices no longer gate the host-memory row loads (p3d_gemv_in_value_n: a device
+// round trip for use2, then the host one).  The caller's wave then reads the staged values by index.
+template <int MR>
+__device__ __forceinline__ void p3d_gemv_in_stage(const GemvFrames& fr, int M, float (*xn)[64]) {
+  const int d = threadIdx.x & 63;
+  if (d < fr.ldraw) {
+    const double mu = fr.mean2[d], sd = fr.std2[d];
+    double xr[MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) xr[r] = r < M ? fr.raw[(int64_t)r * fr.ldraw + d] : 0.0;
+#pragma unroll
+    for (int r = 0; r < MR; ++r) xn[r][d] = p3d_norm_in(xr[r], mu, sd);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// p3d_gemv_in_value_n on the staged values (the same p3d_norm_in values, the same chains)
+__device__ __forceinline__ float p3d_gemv_in_value_s(const GemvArgs& in, const GemvFrames& fr, const float (*xn)[64],
+                                                     const f32x4 (&wv)[2][4], const GemvEpi& e, int r, int f) {
+  float zs = 0.f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 xv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xv[k] = xn[r][fr.use2[16 * g + 4 * q + k] & 63];   // (indices < D2 <= 64)
+      float s = 0.f;
+      s = fmaf(wv[g][q].x, xv.x, s);
+      s = fmaf(wv[g][q].y, xv.y, s);
+      s = fmaf(wv[g][q].z, xv.z, s);
+      s = fmaf(wv[g][q].w, xv.w, s);
+      a[q] = s;
+    }
+    const float t = (a[0] + a[1]) + (a[2] + a[3]);
+    zs += t;
+  }
+  return p3d_gemv_epi(in, e, zs, r, f);
+}
 // the same with x read from in.X (for one feature per lane: no staging)
 __device__ __forceinline__ float p3d_gemv_in_value_g(const GemvArgs& in, const f32x4 (&wv)[2][4], const GemvEpi& e,
                                                      int r, int f) {
@@ -618,6 +661,7 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   constexpr int WV = 16;
   __shared__ float xs[MR * P3D_GEMV_CHAIN_MAXK];
   __shared__ float red[4][WV][MR][16];
+  __shared__ float xn[MR][64];   // p3d_lift: the normalised raw rows (layer 2's wave 0)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
 #ifdef P3D_TRACE   // development builds (tools/trace_chain.py): per workgroup at 8 b: start, input,
@@ -661,7 +705,14 @@ __global__ __launch_bounds__(1024) void k_gemv_chain(GemvChain c) {
   float rv = 0.f;
   if (l == 2 && w == 0) {
     float v0 = 0.f;
-    if (q < M) {
+    if (c.fr.raw && c.fr.ldraw <= 64) {   // (the weights and epilogue operands requested first)
+      f32x4 wv[2][4];
+      GemvEpi ei;
+      p3d_gemv_in_weights(c.in, col, wv);
+      p3d_gemv_epi_load(c.in, 0, col, ei);
+      p3d_gemv_in_stage<MR>(c.fr, M, xn);
+      if (q < M) v0 = p3d_gemv_in_value_s(c.in, c.fr, xn, wv, ei, q, col);
+    } else if (q < M) {
       f32x4 wv[2][4];
       GemvEpi ei;
       p3d_gemv_in_weights(c.in, col, wv);
