@@ -157,7 +157,9 @@ struct p3d_model {
   unsigned hseq = 0;               // last sequence number issued
   unsigned hwait = 0;              // the sequence number the launch being built stores (0: none)
   bool harmed = false;             // the launch just built carries it
-  unsigned* hcnt = nullptr;        // device arrival counter of those launches (zero between them)
+  unsigned* hcnt = nullptr;        // device arrival counter of those launches (zero between them);
+                                   // [8]: p3d_host_signal's counter; [256, 512): the batch <= 4 chain's
+                                   // squared differences (p3d_serve_mse's fused loss)
   // bf16 inference models (cfg5)
   unsigned short* wbf = nullptr;    // packed bf16 weights
   float* aff = nullptr;             // BN-eval affine per BN layer
@@ -622,8 +624,8 @@ extern "C" int p3d_create(const p3d_cfg* cfg_in, p3d_model** out) {
   if (const char* ev = getenv("P3D_FUSE_ADAM")) m->adam_in_wgrad = atoi(ev);
   if (const char* ev = getenv("P3D_WGRAD_MULTI")) m->wgrad_multi = atoi(ev);
   if ((e = hipMalloc(&m->alpha_dev, 64 * sizeof(float))) != hipSuccess) return cleanup(e);
-  if ((e = hipMalloc(&m->hcnt, 64 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
-  if ((e = hipMemset(m->hcnt, 0, 64 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+  if ((e = hipMalloc(&m->hcnt, 512 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
+  if ((e = hipMemset(m->hcnt, 0, 512 * sizeof(unsigned))) != hipSuccess) return cleanup(e);
   if (const char* ev = getenv("P3D_SERVE_GROUPS")) m->serve_groups = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6")) m->serve6 = atoi(ev);
   if (const char* ev = getenv("P3D_SERVE6_MAX_NB")) m->serve6_max_nb = atoi(ev);
@@ -1067,8 +1069,8 @@ static int forward_gemv(p3d_model* m, const float* x, int64_t B, float* y, float
     ch.err = m->xerr;
     if (fr) {
       ch.fr = *fr;
-      ch.out.Y = nullptr;
-      if (ch.fr.hflag) ch.fr.hcount = (ch.out.N + 15) >> 4;   // the output-tile workgroups (p3d_gemv.h)
+      if (ch.fr.out) ch.out.Y = nullptr;   // (p3d_lift: the unNormalizeData'd rows instead)
+      if (ch.fr.hflag || ch.fr.loss) ch.fr.hcount = (ch.out.N + 15) >> 4;   // the output-tile workgroups (p3d_gemv.h)
     }
     {
       ProfScope ps(m, "gemv_chain");
@@ -1377,6 +1379,19 @@ static int serve_impl(p3d_model* m, const float* x, int64_t B, float* y, const f
     return fail(P3D_ERR_HIP, "p3d_serve: an earlier launch failed (not all workgroups resident); p3d_serve_check "
                              "reports and clears it");
   hipStream_t st = (hipStream_t)stream;
+  // batch <= 4 with the loss: the persistent small-batch forward (k_gemv_chain, ~13 us where a 64-row
+  // k_serve6 unit takes ~30) with the loss reduced by its last output workgroup -- still one launch;
+  // y has p3d_forward's bits at this batch, the loss p3d_mse's on that y (stream-ordered with the
+  // model's other batch <= 4 calls: they share workspace slot 0)
+  if (t && loss && B <= m->gemv_maxb) {
+    GemvFrames fr{};
+    fr.tgt = t; fr.loss = loss;
+    fr.hcnt = m->hcnt; fr.sq = reinterpret_cast<float*>(m->hcnt + 256);
+    if (m->hwait) { fr.hflag = m->hflag_dev; fr.hseq = m->hwait; }
+    const int r = forward_gemv(m, x, B, y, 1.0f, 0, 0, 0, 0, st, &fr);
+    if (r == P3D_OK && m->hwait) m->harmed = true;
+    if (r != 1) return r;   // (1: no chain form for this model -- k_serve6 below)
+  }
   const int L = c.linear_size, U = L / 32, NDT = (c.output_size + 15) / 16;
   const int64_t slab = (int64_t)64 * L, PT = (int64_t)4 * NDT * 256;
   hipError_t e;

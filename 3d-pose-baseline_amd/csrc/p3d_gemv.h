@@ -61,20 +61,43 @@ struct GemvFrames {
   // p3d_lift_sync: host-visible completion word (pinned, coherent; null: off), the call's sequence
   // number, a device arrival counter (zero between launches) and the launch's output workgroups
   unsigned* hflag; unsigned* hcnt; unsigned hseq; int hcount;
+  // p3d_serve_mse at B <= 4 (null: off): the targets [M][N] row-major, the loss word, and a device
+  // scratch of the M N squared differences the last output workgroup reduces as k_mse does
+  const float* tgt; float* loss; float* sq;
 };
 
-// The host-completion arrival of one output workgroup (whole workgroup, uniform call): each
-// thread's host-memory stores made system-visible, then one arrival; the last arriver resets the
-// counter and stores the call's sequence number into the host word (system-scope release).
-__device__ __forceinline__ void p3d_host_arrive(const GemvFrames& fr) {
+// The arrival of one output workgroup (whole workgroup, uniform call): each thread's host-memory
+// stores made system-visible, then one arrival on the counter.  The last arriver resets it, with
+// a fused MSE (fr.loss) reduces the squared differences every output workgroup left in fr.sq --
+// k_mse's order (p3d_layers.h: 256 slots, one element each at n <= 256, the same halving tree), so
+// the loss has p3d_mse's bits -- and stores the call's sequence number into the host word
+// (system-scope release; null: no word).  n: the M N squared differences (<= 256: M <= 4, N <= 64).
+__device__ __forceinline__ void p3d_host_arrive(const GemvFrames& fr, int n) {
+  __shared__ int last;
+  __shared__ float part[256];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (system scope: no acquire half, no cache invalidate)
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(fr.hcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((int)prev + 1 == fr.hcount) {
-      __hip_atomic_store(fr.hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(fr.hflag, fr.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    const bool l = (int)prev + 1 == fr.hcount;
+    if (l) __hip_atomic_store(fr.hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l && !fr.loss && fr.hflag) __hip_atomic_store(fr.hflag, fr.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = l;
+  }
+  if (!fr.loss) return;
+  __syncthreads();
+  if (!last) return;   // (uniform)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other output workgroups' squares
+  const int e = threadIdx.x;
+  if (e < 256) part[e] = e < n ? fr.sq[e] : 0.f;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (e < h) part[e] += part[e + h];
+    __syncthreads();
+  }
+  if (e == 0) {
+    *fr.loss = part[0] / (float)n;
+    if (fr.hflag) __hip_atomic_store(fr.hflag, fr.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -465,13 +488,16 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
   const int t1 = t0 + NTO < nto ? t0 + NTO : nto;
   GemvEpi e[NTO];
   f32x4 wf[NTO][GC];
+  float tv[NTO];   // fused MSE (k_gemv_chain): the targets, requested with the other epilogue operands
 #pragma unroll
   for (int u = 0; u < NTO; ++u) {
     const int t = t0 + u;
+    tv[u] = 0.f;
     if (t >= t1) break;
     const int col = 16 * t + i, cc = col < o.N ? col : o.N - 1;
     e[u].ctr = o.ctr;
     if (w == 0 && q < M) p3d_gemv_epi_load(o, q, cc, e[u]);
+    if (NTO == 1 && f.fr.tgt && w == 0 && q < M) tv[u] = f.fr.tgt[(int64_t)q * o.N + cc];
     p3d_gemv_preload<GC>((const f32x4*)o.Wf + (int64_t)t * ngK * 64 + lane, gb, ge, wf[u]);
   }
 #pragma unroll
@@ -479,6 +505,7 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
     if (t0 + u >= t1) break;
     p3d_pin<GC>(wf[u]);
     p3d_pin_epi(e[u]);
+    asm volatile("" : "+v"(tv[u]));
   }
   // unNormalizeData's operands depend on no input: waves 1.. write the unused dimensions
   // ((float) 0 * std + mean) and stage the used columns' index / std / mean in LDS while the
@@ -548,10 +575,15 @@ __device__ __forceinline__ void p3d_gemv_fold_out(const GemvFold& f, unsigned ta
       if (col < o.N) {
         if (o.Y) o.Y[(int64_t)q * o.ldy + col] = y;
         if (f.fr.out) f.fr.out[(int64_t)q * f.fr.D3 + od[col]] = p3d_unnorm_out(y, osd[col], omu[col]);
+        if (NTO == 1 && f.fr.tgt) {   // k_mse's element term: d = y - t, d * d
+          const float d = y - tv[u];
+          f.fr.sq[q * o.N + col] = d * d;
+        }
       }
     }
   }
-  if (f.fr.hflag) p3d_host_arrive(f.fr);
+  // (frames, the completion word and the fused loss: k_gemv_chain's one-tile form only)
+  if (NTO == 1 && (f.fr.hflag || f.fr.loss)) p3d_host_arrive(f.fr, M * o.N);
 }
 
 // A hidden layer as k_gemv<MR, WV, GC> (the same bits), with the input layer folded in ahead of it

@@ -835,7 +835,7 @@ class LinearModel(object):
         st["hx_np"], st["ht_np"] = st["hx"].numpy(), st["ht"].numpy()
         st["hy_np"], st["hl_np"] = st["hy"].numpy(), st["hl"].numpy()
         if not training:
-            # (batches the one-launch p3d_serve_mse_sync path does not take: B <= 4, B > 2048, bf16)
+            # (batches the one-launch p3d_serve_mse_sync path does not take: B > 2048, bf16)
             signal = os.environ.get("P3D_HOST_WAIT", "1") != "0"
             if signal:
                 # round 6: the forward reads x from the pinned block and writes y into coherent host
@@ -924,14 +924,15 @@ class LinearModel(object):
     def _serve_step_state(self, B):
         """Pinned buffers of the one-launch evaluation step (p3d_serve_mse): [x | t] in, y out and
         the loss word, all read and written by the kernel directly (mapped host memory), with the
-        launch's ctypes arguments bound once.  None when no k_serve6 form covers B (the library
+        launch's ctypes arguments bound once (B <= 4: the library's persistent small-batch forward,
+        its last output workgroup reducing the loss).  None when no k_serve6 form covers B (the library
         says so once: P3D_ERR_ARG) -- the cached-graph path runs then."""
         st = self._serve_steps.get(B, False)
         if st is not False:
             return st
         torch = self.torch
         st = None
-        if (not self.bf16 and 4 < B <= 32 * 64 and self.linear_size % 128 == 0 and self.num_layers > 0
+        if (not self.bf16 and 0 < B <= 32 * 64 and self.linear_size % 128 == 0 and self.num_layers > 0
                 and os.environ.get("P3D_STEP_SERVE", "1") != "0"):
             import ctypes
             f32 = torch.float32

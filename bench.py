@@ -914,9 +914,10 @@ def bench_api(args, rank, world, n_infer=300, n_train=100):
         model.step(None, x1, t1, 1.0, isTraining=False)
     dt = time.perf_counter() - t0
     out["eval_b1"] = {"us_per_call": round(1e6 * dt / n1, 2), "unit": "us",
-                      "note": "LinearModel.step() at batch 1 from numpy: one replayed HIP graph of the persistent "
-                              "batch-1 forward (k_gemv_chain, x read from pinned memory, y written to coherent host "
-                              "memory), MSE, and a host signal the host waits on"}
+                      "note": "LinearModel.step() at batch 1 from numpy: one p3d_serve_mse_sync call -- the persistent "
+                              "batch-1 forward (k_gemv_chain) reads x / t from pinned memory, writes y there, its last "
+                              "output workgroup reduces the loss (k_mse's order) and stores a completion word the host "
+                              "waits on"}
     # device time of the batch-1 forward itself (k_gemv layers): a HIP graph of 50 forwards
     # replayed back to back (kernels + the dependent boundaries between them), and the hidden
     # layer's dispatch-attached duration against its weight stream

@@ -138,8 +138,12 @@ int p3d_serve(p3d_model* m, const float* x, int64_t B, float* y, void* stream);
  * step(), :239-245) fused into the launch: *loss = mean((y - t)^2) over B x output_size, t [B,
  * output_size] row-major.  x, y, t and loss may be pinned (mapped) host memory: the kernel reads
  * and writes them directly, so LinearModel.step(isTraining=False) is ONE launch from numpy.
- * P3D_ERR_ARG where no k_serve6 form covers the launch (> 32 batch-64 steps, or a model shape
- * it is not built for): the caller uses p3d_serve + p3d_mse there. */
+ * B <= 4 (the batch-1 front end's evaluation): the persistent small-batch forward p3d_forward
+ * runs at that batch, its last output workgroup reducing the loss -- y then has p3d_forward's
+ * bits and *loss p3d_mse's on that y; it shares workspace slot 0 with the model's other batch
+ * <= 4 calls, so keep those on one stream.  P3D_ERR_ARG where no form covers the launch (> 32
+ * batch-64 steps, or a model shape it is not built for): the caller uses p3d_serve + p3d_mse
+ * there. */
 int p3d_serve_mse(p3d_model* m, const float* x, int64_t B, float* y, const float* t, float* loss, void* stream);
 /* p3d_serve_mse that returns once y and *loss hold the results, for outputs in pinned host memory
  * (the reference's session.run returns its fetches: src/linear_model.py:239-245).  The launch's last

@@ -444,13 +444,13 @@ def test_serve_mse_fused_loss_and_pinned_io(B, max_norm, p14):
 
 
 def test_step_eval_one_launch_path_and_fallback():
-    """LinearModel.step(isTraining=False) from numpy: B in (4, 2048] runs ONE p3d_serve_mse launch
-    on pinned buffers; B = 3 (the batch <= 4 chain) and B = 2100 (> 32 batch-64 steps: no k_serve6
-    form, the library answers P3D_ERR_ARG once) take the cached-graph path.  Every path equals the
-    oracle's eval step (outputs 2e-5, loss 1e-5 relative)."""
+    """LinearModel.step(isTraining=False) from numpy: B <= 2048 runs ONE p3d_serve_mse launch on
+    pinned buffers (B = 3: the batch <= 4 chain with its fused loss); B = 2100 (> 32 batch-64 steps:
+    no k_serve6 form, the library answers P3D_ERR_ARG once) takes the cached-graph path.  Every path
+    equals the oracle's eval step (outputs 2e-5, loss 1e-5 relative)."""
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     st, m = make(cfg, max_batch=4096)
-    for B, one_launch in ((64, True), (300, True), (3, False), (2100, False)):
+    for B, one_launch in ((64, True), (300, True), (3, True), (2100, False)):
         rng = np.random.default_rng(B)
         x, t = rng.standard_normal((B, 32)), rng.standard_normal((B, 48))
         for _ in range(2):
@@ -462,11 +462,12 @@ def test_step_eval_one_launch_path_and_fallback():
     m.close()
 
 
-@pytest.mark.parametrize("B", [64, 37, 300, 1280])
+@pytest.mark.parametrize("B", [64, 37, 300, 1280, 1, 4])
 def test_serve_mse_sync_returns_with_results_in_host_memory(B):
     """p3d_serve_mse_sync (round 6): returns once y and the loss are in the pinned buffers -- the
     launch's last output tile stores a completion word the host waits on (B = 1280: the pair form,
-    which carries no word, waits on the stream instead).  Read straight after the call, with no
+    which carries no word, waits on the stream instead; B = 1, 4: the batch <= 4 chain, whose last
+    output workgroup reduces the loss before it stores the word).  Read straight after the call, with no
     synchronize, 12 calls on fresh inputs each equal p3d_serve_mse's results on the same inputs
     (stream-synchronised) bit for bit -- a result of the previous call would show as a mismatch."""
     import ctypes
@@ -500,24 +501,66 @@ def test_serve_mse_sync_returns_with_results_in_host_memory(B):
     m.close()
 
 
-@pytest.mark.parametrize("B", [64, 3])
+@pytest.mark.parametrize("B,p14,max_norm", [(1, False, False), (3, False, False), (4, True, False),
+                                            (2, False, True)])
+def test_serve_mse_small_batch_is_forward_and_mse(B, p14, max_norm):
+    """p3d_serve_mse at B <= 4 (round 6): the persistent small-batch forward with the loss reduced by
+    its last output workgroup in k_mse's order.  y equals p3d_forward's at that batch and the loss
+    equals p3d_mse's on that y, bit for bit, over 6 calls on fresh pinned inputs, and both match the
+    oracle's eval step (src/linear_model.py:129)."""
+    import ctypes
+    import _p3d
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True, max_norm=max_norm,
+                      predict_14=p14)
+    st, m = make(cfg)
+    D = cfg.output_size
+    c = ctypes.c_void_p
+    lib = _p3d.lib()
+    hx = torch.empty((B, 32), dtype=torch.float32).pin_memory()
+    ht = torch.empty((B, D), dtype=torch.float32).pin_memory()
+    hy = torch.empty((B, D), dtype=torch.float32).pin_memory()
+    hl = torch.zeros(4, dtype=torch.float32).pin_memory()
+    dl = torch.zeros(4, dtype=torch.float32, device="cuda")
+    rng = np.random.default_rng(B + 91)
+    for it in range(6):
+        hx.copy_(torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)))
+        ht.copy_(torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)))
+        _p3d.check(lib.p3d_serve_mse(m._h, c(hx.data_ptr()), B, c(hy.data_ptr()), c(ht.data_ptr()),
+                                     c(hl.data_ptr()), c(_p3d.stream_handle())), "p3d_serve_mse")
+        torch.cuda.synchronize()
+        yd = m.forward_device(hx.cuda())
+        td = ht.cuda()
+        _p3d.check(lib.p3d_mse(c(yd.data_ptr()), c(td.data_ptr()), B, D, c(dl.data_ptr()), None,
+                               c(_p3d.stream_handle())), "p3d_mse")
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(hy.numpy(), yd.cpu().numpy(), err_msg="call %d" % it)
+        assert float(hl[0]) == float(dl[0].cpu()), (it, float(hl[0]), float(dl[0].cpu()))
+    m.check_errors()
+    rl, ro = ref_mlp.eval_step(st, hx.numpy().astype(np.float64), ht.numpy().astype(np.float64))
+    close(hy.numpy(), ro)
+    assert abs(float(hl[0]) - rl) <= 1e-5 * max(1.0, abs(rl)), (float(hl[0]), rl)
+    m.close()
+
+
+@pytest.mark.parametrize("B", [64, 3, 2100])
 def test_step_eval_host_wait_equals_stream_sync(monkeypatch, B):
     """LinearModel.step(isTraining=False) through the host-wait forms (default) and through the
-    stream-synchronised ones (P3D_HOST_WAIT=0): B = 64 is one p3d_serve_mse_sync call vs
-    p3d_serve_mse + a synchronize; B = 3 (the batch <= 4 chain) is the captured forward + MSE whose
-    last node is p3d_host_signal, reading x / t from pinned memory and writing y / the loss into
-    coherent host memory, vs the copy-node graph + a synchronize.  10 steps on fresh inputs, the
-    same outputs and loss bit for bit, step by step, and the oracle's eval step."""
+    stream-synchronised ones (P3D_HOST_WAIT=0): B = 64 and B = 3 (the batch <= 4 chain with its
+    fused loss) are one p3d_serve_mse_sync call vs p3d_serve_mse + a synchronize; B = 2100 (no
+    one-launch form) is the captured forward + MSE whose last node is p3d_host_signal, reading x / t
+    from pinned memory and writing y / the loss into coherent host memory, vs the copy-node graph +
+    a synchronize.  10 steps on fresh inputs, the same outputs and loss bit for bit, step by step,
+    and the oracle's eval step."""
     cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
     res = {}
     for hw in ("1", "0"):
         monkeypatch.setenv("P3D_HOST_WAIT", hw)
-        st, m = make(cfg)
+        st, m = make(cfg, max_batch=max(B, 64))
         rng = np.random.default_rng(77)
         xs = [(rng.standard_normal((B, 32)), rng.standard_normal((B, 48))) for _ in range(10)]
         res[hw] = [m.step(None, x, t, 1.0, isTraining=False) for x, t in xs]
-        if B == 64:
-            assert m._serve_steps[64]["sync"] == (hw == "0")
+        if B <= 2048:
+            assert m._serve_steps[B]["sync"] == (hw == "0")
         else:
             assert bool(m._host_steps[(False, B, 1.0, m.lr0, m.seed)].get("signal")) == (hw == "1")
         m.close()

@@ -43,6 +43,8 @@ def main():
     t = rng.standard_normal((64, 48))
     out = {}
     out["step_eval_b64"] = med(lambda: model.step(None, x, t, 1.0, isTraining=False))
+    x1, t1 = x[:1], t[:1]
+    out["step_eval_b1"] = med(lambda: model.step(None, x1, t1, 1.0, isTraining=False))
     st = model._host_step_state(False, 64, 1.0)
 
     def replay_sync(st_):
