@@ -501,6 +501,35 @@ def test_serve_mse_sync_returns_with_results_in_host_memory(B):
     m.close()
 
 
+@pytest.mark.parametrize("knob", ["P3D_GEMV_CHAIN", "P3D_GEMV_MAXB"])
+def test_serve_mse_small_batch_without_the_chain(knob, monkeypatch):
+    """p3d_serve_mse(_sync) at B = 3 on a model without the batch <= 4 chain (P3D_GEMV_CHAIN=0: the
+    forward's fold form, which carries no fused loss; P3D_GEMV_MAXB=0: no small-batch forms) falls
+    through to k_serve6: one launch still, y equals p3d_serve's bit for bit, y and the loss match the
+    oracle's eval step, and the sync call's results are in host memory when it returns."""
+    import ctypes
+    import _p3d
+    monkeypatch.setenv(knob, "0")
+    cfg = ref_mlp.Cfg(linear_size=1024, num_layers=2, residual=True, batch_norm=True)
+    st, m = make(cfg)
+    B, c, lib = 3, ctypes.c_void_p, _p3d.lib()
+    rng = np.random.default_rng(29)
+    hx = torch.from_numpy(rng.standard_normal((B, 32)).astype(np.float32)).pin_memory()
+    ht = torch.from_numpy(rng.standard_normal((B, 48)).astype(np.float32)).pin_memory()
+    hy = torch.empty((B, 48), dtype=torch.float32).pin_memory()
+    hl = torch.zeros(4, dtype=torch.float32).pin_memory()
+    _p3d.check(lib.p3d_serve_mse_sync(m._h, c(hx.data_ptr()), B, c(hy.data_ptr()), c(ht.data_ptr()),
+                                      c(hl.data_ptr()), c(_p3d.stream_handle())), "p3d_serve_mse_sync")
+    got_y, got_l = hy.numpy().copy(), float(hl[0])
+    torch.cuda.synchronize()
+    m.serve_check()
+    np.testing.assert_array_equal(got_y, m.serve_device(hx.cuda()).cpu().numpy())
+    rl, ro = ref_mlp.eval_step(st, hx.numpy().astype(np.float64), ht.numpy().astype(np.float64))
+    close(got_y, ro)
+    assert abs(got_l - rl) <= 1e-5 * max(1.0, abs(rl)), (got_l, rl)
+    m.close()
+
+
 @pytest.mark.parametrize("B,p14,max_norm", [(1, False, False), (3, False, False), (4, True, False),
                                             (2, False, True)])
 def test_serve_mse_small_batch_is_forward_and_mse(B, p14, max_norm):
