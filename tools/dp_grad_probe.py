@@ -5,7 +5,6 @@ GPU, L = 1024, B = 64 per rank) vs the oracle's per-replica backward at the same
 """
 import json
 import os
-import socket
 import sys
 
 import numpy as np
@@ -19,11 +18,8 @@ sys.path.insert(0, ROOT)
 
 
 def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    import dist_utils   # the shared helper (3d-pose-baseline_amd/dist_utils.py)
+    return dist_utils.free_port()
 
 
 def worker(rank, world, port, out, L, B, keep):
